@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""bench.py -- GCUPS of the batched Smith-Waterman scoring path on MI355X.
+
+Workload (BASELINE.json configs[1], "config 2"): 10,000 synthetic 150 bp
+reads x 300 bp reference windows, linear gap (+2/-1/-2), score-only, inputs
+resident in HBM.  One step = one pass of the hot path (msw_align_batch_device:
+the hand-written gfx950 kernel through the C ABI) over the batch.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank scores its
+own fresh 10k-pair shard (weak scaling, no data-path collective); after the
+timed region the scores are gathered to rank 0 over RCCL (the only collective,
+as north_star prescribes).  value = cells of all ranks / max-over-ranks time.
+
+Extra fields: ``roofline`` (HBM, as north_star asks; algorithmic bytes per
+launch / average launch time from HIP events on the launch stream), ``valu``
+(the binding VALU-integer ceiling), ``cpu_baseline`` (the C oracle on the
+host cores, bounded sample, rank 0 only) and ``parity`` (GPU vs oracle on
+that sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Per-gfx950 constants (/opt/skills/guides/MI355X_MICROARCH.md, chip table).
+HBM_PEAK_GBPS = 8000.0
+VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9          # 7.86e13 32-bit lane-ops/s
+OPS_PER_CELL_PAIR = {"linear": 6.5, "linear_coords": 9.5, "affine": 10.5, "affine_coords": 13.5}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
+                    help="BASELINE config whose batch shape is timed (2 = the metric's)")
+    ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU work for the cpu_baseline sample (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def load_pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel_prefix)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+
+    import torch  # first: libmsw.so then binds to the same HIP runtime as torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from mini_parallel_amd import Context, Scoring
+    from mini_parallel_amd.synthetic import config_batch
+
+    cfg = args.config
+    scoring = {2: Scoring(), 3: Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True),
+               5: Scoring()}[cfg]
+    kind = ("affine" if scoring.affine else "linear") + ("_coords" if scoring.want_coords else "")
+    n_pairs = args.pairs or {2: 10_000, 3: 1_000_000, 5: 100_000}[cfg]
+    batch = config_batch(cfg, n_pairs=n_pairs, seed_offset=1000 * rank)
+    if cfg == 5:  # device path takes one launch: sort by length so waves are tight
+        order = np.lexsort((batch.win_len, batch.read_len))
+        batch = batch.__class__(batch.reads[order], batch.read_len[order], batch.wins[order],
+                                batch.win_len[order], batch.pos[order])
+    cells = batch.cells
+
+    def to_dev(a, dt=None):
+        a = np.ascontiguousarray(a if dt is None else a.view(dt))
+        return torch.from_numpy(a).to(dev)
+
+    reads, wins = to_dev(batch.reads), to_dev(batch.wins)
+    rlen, wlen = to_dev(batch.read_len, np.int16), to_dev(batch.win_len, np.int16)
+    score = torch.zeros(batch.n_pairs, dtype=torch.int32, device=dev)
+    ei = torch.zeros(batch.n_pairs, dtype=torch.int16, device=dev)
+    ej = torch.zeros(batch.n_pairs, dtype=torch.int16, device=dev)
+    max_m, max_n = int(batch.read_len.max()), int(batch.win_len.max())
+
+    ctx = Context(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step():
+        ctx.align_batch_device(reads.data_ptr(), rlen.data_ptr(), wins.data_ptr(), wlen.data_ptr(),
+                               batch.reads.shape[1], batch.wins.shape[1], batch.n_pairs,
+                               score.data_ptr(), max_m, max_n, scoring, ei.data_ptr(),
+                               ej.data_ptr(), sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    kern_ms = ev0.elapsed_time(ev1)
+
+    t = torch.tensor([wall_ms, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_ms, kern_ms = float(t[0]), float(t[1])
+
+    # Final score gather to rank 0 over RCCL (outside the timed region).
+    gathered = None
+    if world > 1:
+        parts = [torch.zeros_like(score) for _ in range(world)]
+        dist.all_gather(parts, score)
+        gathered = sum(int(p.numel()) for p in parts)
+
+    if rank == 0:
+        gpu_scores = score.cpu().numpy()
+        gpu_i, gpu_j = ei.cpu().numpy(), ej.cpu().numpy()
+        value = world * cells * args.steps / (wall_ms * 1e-3) / 1e9
+        ms_per_step = wall_ms / args.steps
+        avg_launch_s = kern_ms * 1e-3 / args.steps
+        alg_bytes = int(batch.read_len.astype(np.int64).sum() + batch.win_len.astype(np.int64).sum()
+                        + batch.n_pairs * (8 if scoring.want_coords else 4))
+        achieved = alg_bytes / avg_launch_s / 1e9
+        kernel_gcups = cells / avg_launch_s / 1e9
+        valu_ceiling = VALU_LANE_OPS * 2 / OPS_PER_CELL_PAIR[kind] / 1e9
+        traffic = load_pmc_traffic(f"sw_{'affine' if scoring.affine else 'linear'}_kernel")
+
+        cpu = None
+        parity = None
+        if args.cpu_seconds > 0:
+            from oracle import oracle_lib
+            oracle_lib.build()
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            kw = dict(match=scoring.match, mismatch=scoring.mismatch, gap_open=scoring.gap_open,
+                      gap_extend=scoring.gap_extend, affine=scoring.affine, threads=threads)
+            # calibrate on a small sample, then size the sample to ~cpu_seconds
+            n0 = min(batch.n_pairs, 64 * threads)
+            ts = time.perf_counter()
+            oracle_lib.sw_batch(batch.reads[:n0], batch.read_len[:n0], batch.wins[:n0],
+                                batch.win_len[:n0], **kw)
+            rate = n0 / max(time.perf_counter() - ts, 1e-6)
+            ns = int(min(batch.n_pairs, max(n0, rate * args.cpu_seconds)))
+            ts = time.perf_counter()
+            cs, ci, cj = oracle_lib.sw_batch(batch.reads[:ns], batch.read_len[:ns], batch.wins[:ns],
+                                             batch.win_len[:ns], **kw)
+            dt = time.perf_counter() - ts
+            scells = int((batch.read_len[:ns].astype(np.int64) * batch.win_len[:ns]).sum())
+            cpu = {"value": round(scells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads,
+                   "kind": "port",
+                   "sample": f"first {ns} of the {batch.n_pairs} timed pairs ({scells} cells, "
+                             f"{dt:.1f} s), oracle/sw_oracle.c scalar, {threads} threads"}
+            mism = int((cs != gpu_scores[:ns]).sum())
+            if scoring.want_coords:
+                mism += int(((ci != gpu_i[:ns]) | (cj != gpu_j[:ns])).sum())
+            parity = {"checked_pairs": ns, "mismatches": mism, "bit_exact": mism == 0}
+
+        line = {
+            "metric": "GCUPS (billion cell updates/s) on 150bp reads, 1/2/4/8 MI355X; bit-exact scores",
+            "value": round(value, 2),
+            "unit": "GCUPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic (seeded genome, 1% subs, 0.1% indels, 0.05% N, 10% unrelated reads)",
+            "config": {"workload": f"config{cfg}: {batch.n_pairs} pairs/GPU, reads {int(batch.read_len.min())}-"
+                                   f"{max_m} bp x windows {int(batch.win_len.min())}-{max_n} bp, "
+                                   f"{kind.replace('_', '+')}, HBM-resident",
+                       "pairs_per_gpu": batch.n_pairs, "cells_per_gpu_step": cells,
+                       "parallelism": f"dp{world}", "kernel": f"sw_{kind}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                         "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+            "valu": {"binding": True, "kernel_gcups": round(kernel_gcups, 1),
+                     "ceiling_gcups": round(valu_ceiling, 1),
+                     "frac": round(kernel_gcups / valu_ceiling, 4),
+                     "ops_per_packed_cell_pair": OPS_PER_CELL_PAIR[kind]},
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "gathered_scores": gathered,
+        }
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * msw.h -- C ABI of the MI355X-native batched Smith-Waterman scorer.
+ *
+ * This is the drop-in boundary for the `smith_waterman` crate's scoring path
+ * (bmwoolf/mini_parallel, package `rustseq_mini`).  The reference has no FFI
+ * layer of its own (binary-only crate, Cargo.toml:7-17); each entry point
+ * below names the Rust item it replaces (file:line under smith_waterman/src/).
+ * A Rust crate binds it with a plain `extern "C"` block.
+ *
+ * Contract
+ *  - C99 POD only; no C++ exceptions cross this boundary; every int-returning
+ *    call returns MSW_OK (0) or a negative MSW_E* code, and msw_last_error()
+ *    returns the thread-local message (mirrors Result<_, String>, e.g.
+ *    aligner.rs:452-455).
+ *  - One msw_ctx per GPU, used by one host thread at a time.  Contexts on
+ *    different GPUs run concurrently.  The library owns all device memory and
+ *    streams; the caller owns every host array it passes in.
+ *  - Byte semantics follow the reference kernel: substitution is byte
+ *    equality (smith_waterman.cl:43,114), case-sensitive, 'N' == 'N'.
+ *  - Score = global max cell, >= 0.  Coordinates = 0-based (i in read, j in
+ *    window) of the best cell, smallest i then smallest j on ties; (-1,-1)
+ *    when the score is 0 or the pair is empty.
+ *  - Supported by the GPU kernels: read length <= 256, window length <= 4096,
+ *    1 <= match <= 64, mismatch in [match-64, match], gaps >= 0 and
+ *    match * (min(read,window)+1) < 31744.  Anything else -> MSW_E_RANGE.
+ *    There is no CPU fallback: without a usable GPU every call fails.
+ */
+#ifndef MSW_H
+#define MSW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSW_OK 0
+#define MSW_E_INVALID (-1)   /* bad argument / NULL pointer              */
+#define MSW_E_RANGE (-2)     /* length or scoring outside kernel limits  */
+#define MSW_E_DEVICE (-3)    /* HIP runtime / launch failure             */
+#define MSW_E_NODEVICE (-4)  /* no GPU (is_gpu_available() == false)     */
+#define MSW_E_NOMEM (-5)     /* device or pinned allocation failed       */
+
+/* Replaces GpuDevice{name, memory_gb, max_work_group_size} (gpu.rs:17-22). */
+typedef struct {
+    char name[256];
+    uint64_t mem_bytes;
+    uint64_t mem_free_bytes;    /* hipMemGetInfo; replaces system_info.rs:236-243 */
+    uint32_t max_wg;            /* max work-group size (gpu.rs:62)           */
+    uint32_t cu_count;
+    char arch[64];              /* e.g. "gfx950"                             */
+} msw_device_info_t;
+
+/* Scoring.  Reference constants: match +2, mismatch -1, gap 2
+ * (smith_waterman.cl:5-7).  Linear gap: affine = 0, gap_extend = gap penalty,
+ * gap_open ignored.  Affine (Gotoh): a gap of length k costs
+ * gap_open + k * gap_extend.  want_coords = 1 fills end_i / end_j. */
+typedef struct {
+    int32_t match;
+    int32_t mismatch;
+    int32_t gap_open;
+    int32_t gap_extend;
+    int32_t affine;
+    int32_t want_coords;
+} msw_scoring_t;
+
+/* A padded SoA batch: pair p uses reads[p*read_stride ..][0, read_len[p]) and
+ * wins[p*win_stride ..][0, win_len[p]).  In msw_align_batch the pointers are
+ * host memory (pageable or msw_host_alloc'ed); in msw_align_batch_device they
+ * are device memory.  Replaces the Vec<String> chunk handed to the loader
+ * callback (aligner.rs:107-108, :128-147). */
+typedef struct {
+    const uint8_t* reads;
+    const uint8_t* wins;
+    const uint16_t* read_len;
+    const uint16_t* win_len;
+    uint32_t read_stride;
+    uint32_t win_stride;
+    uint64_t n_pairs;
+} msw_batch_t;
+
+/* Caller-owned outputs (host in msw_align_batch, device in _device).
+ * end_i / end_j may be NULL when want_coords == 0. */
+typedef struct {
+    int32_t* score;
+    int16_t* end_i;
+    int16_t* end_j;
+} msw_out_t;
+
+typedef struct msw_ctx msw_ctx;
+
+/* gpu.rs:33-45 is_gpu_available / gpu.rs:48-94 get_gpu_devices. */
+int msw_device_count(int* n);
+int msw_device_info(int ordinal, msw_device_info_t* out);
+
+/* gpu.rs:97-132 get_opencl_context/init_opencl: one context per device with a
+ * compute stream, a copy stream and double-buffered pinned staging. */
+int msw_ctx_create(int ordinal, msw_ctx** out);
+void msw_ctx_destroy(msw_ctx* ctx);
+
+/* Batched scoring from host memory, synchronous.  Streams the batch through
+ * pinned staging in chunks of `chunk_pairs` (0 = GPU_CHUNK_SIZE_READS env, or
+ * 65536) with H2D copies on the copy stream overlapped with the kernels.
+ * Replaces the per-chunk gpu_align loop of aligner.rs:269-289 / :390-398. */
+int msw_align_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch,
+                    msw_out_t* out, uint64_t chunk_pairs);
+
+/* Same, asynchronous: returns a ticket; host arrays must stay alive and
+ * unmodified until msw_wait(ticket) returns. */
+int msw_align_batch_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch,
+                          msw_out_t* out, uint64_t chunk_pairs, uint64_t* ticket);
+int msw_wait(msw_ctx* ctx, uint64_t ticket);
+
+/* Device-resident batch: pointers in `batch` and `out` are device memory.
+ * Enqueued on `stream` (a hipStream_t; NULL = the context's compute stream),
+ * no host synchronisation.  max_read_len / max_win_len bound the batch (the
+ * caller knows them; they select the kernel instance and the LDS size). */
+int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch,
+                           msw_out_t* out, uint32_t max_read_len, uint32_t max_win_len,
+                           void* stream);
+
+/* == gpu_align(seq1, seq2, device) (aligner.rs:410-532): the kernel the
+ * reference actually launches (smith_waterman.cl:11-71) with its host geometry
+ * W = min(max_wg, 1024) (aligner.rs:422), G = min(ceil(L/W), max_groups)
+ * (:423-424; reference max_groups = 1,000,000, gpu.rs:10), L = min(n1, n2),
+ * L == 0 -> 0 (:414-416), L > 1,024,000,000 or > 0.8*mem/3 -> MSW_E_RANGE
+ * (:436-456).  wg == 0 -> device max work-group size capped at 1024. */
+int msw_align_compat(msw_ctx* ctx, const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2,
+                     uint32_t wg, uint32_t max_groups, int32_t* score);
+
+/* Pinned host memory (hipHostMalloc); replaces USE_PINNED_MEMORY /
+ * alloc_host_ptr (aligner.rs:466-475). */
+void* msw_host_alloc(size_t bytes);
+void msw_host_free(void* p);
+
+/* Device memory helpers for callers that keep batches resident in HBM. */
+void* msw_dev_alloc(msw_ctx* ctx, size_t bytes);
+void msw_dev_free(msw_ctx* ctx, void* p);
+int msw_memcpy_h2d(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
+int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
+int msw_synchronize(msw_ctx* ctx);
+
+/* Thread-local message of the last failing call on this thread. */
+const char* msw_last_error(void);
+
+/* Library version string (also names the compiled GPU target). */
+const char* msw_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSW_H */

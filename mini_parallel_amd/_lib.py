@@ -1,0 +1,117 @@
+"""ctypes binding of the in-tree C ABI library ``libmsw.so`` (include/msw.h).
+
+There is no CPU fallback: if the HIP library is missing or no GPU is present,
+every call raises :class:`MswError` (the reference likewise refuses to run
+without ``--gpu``, main.rs:160-163).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmsw.so")
+
+MSW_OK = 0
+MSW_E_INVALID = -1
+MSW_E_RANGE = -2
+MSW_E_DEVICE = -3
+MSW_E_NODEVICE = -4
+MSW_E_NOMEM = -5
+
+# Every symbol include/msw.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "msw_device_count", "msw_device_info", "msw_ctx_create", "msw_ctx_destroy",
+    "msw_align_batch", "msw_align_batch_async", "msw_wait", "msw_align_batch_device",
+    "msw_align_compat", "msw_host_alloc", "msw_host_free", "msw_dev_alloc", "msw_dev_free",
+    "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
+)
+
+
+class MswError(RuntimeError):
+    """A failing msw_* call; mirrors the reference's ``Err(String)``."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+class ScoringT(ctypes.Structure):
+    _fields_ = [("match", ctypes.c_int32), ("mismatch", ctypes.c_int32),
+                ("gap_open", ctypes.c_int32), ("gap_extend", ctypes.c_int32),
+                ("affine", ctypes.c_int32), ("want_coords", ctypes.c_int32)]
+
+
+class BatchT(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_void_p), ("wins", ctypes.c_void_p),
+                ("read_len", ctypes.c_void_p), ("win_len", ctypes.c_void_p),
+                ("read_stride", ctypes.c_uint32), ("win_stride", ctypes.c_uint32),
+                ("n_pairs", ctypes.c_uint64)]
+
+
+class OutT(ctypes.Structure):
+    _fields_ = [("score", ctypes.c_void_p), ("end_i", ctypes.c_void_p),
+                ("end_j", ctypes.c_void_p)]
+
+
+class DeviceInfoT(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 256), ("mem_bytes", ctypes.c_uint64),
+                ("mem_free_bytes", ctypes.c_uint64), ("max_wg", ctypes.c_uint32),
+                ("cu_count", ctypes.c_uint32), ("arch", ctypes.c_char * 64)]
+
+
+_lib = None
+
+
+def _declare(L):
+    P = ctypes.c_void_p
+    I = ctypes.c_int
+    sigs = {
+        "msw_device_count": (I, [ctypes.POINTER(I)]),
+        "msw_device_info": (I, [I, ctypes.POINTER(DeviceInfoT)]),
+        "msw_ctx_create": (I, [I, ctypes.POINTER(P)]),
+        "msw_ctx_destroy": (None, [P]),
+        "msw_align_batch": (I, [P, ctypes.POINTER(ScoringT), ctypes.POINTER(BatchT),
+                                ctypes.POINTER(OutT), ctypes.c_uint64]),
+        "msw_align_batch_async": (I, [P, ctypes.POINTER(ScoringT), ctypes.POINTER(BatchT),
+                                      ctypes.POINTER(OutT), ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64)]),
+        "msw_wait": (I, [P, ctypes.c_uint64]),
+        "msw_align_batch_device": (I, [P, ctypes.POINTER(ScoringT), ctypes.POINTER(BatchT),
+                                       ctypes.POINTER(OutT), ctypes.c_uint32, ctypes.c_uint32, P]),
+        "msw_align_compat": (I, [P, P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.c_uint32,
+                                 ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]),
+        "msw_host_alloc": (P, [ctypes.c_size_t]),
+        "msw_host_free": (None, [P]),
+        "msw_dev_alloc": (P, [P, ctypes.c_size_t]),
+        "msw_dev_free": (None, [P, P]),
+        "msw_memcpy_h2d": (I, [P, P, ctypes.c_size_t]),
+        "msw_memcpy_d2h": (I, [P, P, ctypes.c_size_t]),
+        "msw_synchronize": (I, [P]),
+        "msw_last_error": (ctypes.c_char_p, []),
+        "msw_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load libmsw.so (raises MswError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MswError(MSW_E_NODEVICE,
+                           f"{LIB_PATH} is not built: run `make -C mini_parallel_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != MSW_OK:
+        msg = lib().msw_last_error()
+        raise MswError(rc, msg.decode() if msg else f"msw error {rc}")

@@ -1,0 +1,246 @@
+"""Host-side mirror of the reference's align/score API over the C ABI.
+
+Reference interface (smith_waterman/src/), same names, argument meaning and
+error behaviour (errors raise :class:`MswError`, the ``Err(String)`` analogue):
+
+  gpu.rs:9-10        GPU_WORK_GROUP_SIZE, GPU_MAX_WORK_GROUPS
+  gpu.rs:17-30       GpuDevice, GpuAlignmentResult
+  gpu.rs:33-94       is_gpu_available, get_gpu_devices
+  gpu.rs:97-109      get_opencl_context  -> get_context (one Context per GPU)
+  aligner.rs:9-15    get_chunk_size_reads
+  aligner.rs:365-373 gpu_align_chunk_self
+  aligner.rs:410-532 gpu_align            (legacy kernel semantics, K0)
+
+New batched API (north_star): ``Context.align_batch`` (host arrays, pinned
+async staging) and ``Context.align_batch_device`` (HBM-resident batches), both
+calling the hand-written gfx950 kernels through include/msw.h.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import (MSW_E_INVALID, BatchT, DeviceInfoT, MswError, OutT, ScoringT, check, lib)
+
+GPU_WORK_GROUP_SIZE = 1024          # gpu.rs:9
+GPU_MAX_WORK_GROUPS = 1_000_000     # gpu.rs:10
+
+
+@dataclass
+class GpuDevice:
+    """gpu.rs:17-22, plus the HIP ordinal / CU count / arch."""
+    name: str
+    memory_gb: float
+    max_work_group_size: int
+    ordinal: int = 0
+    cu_count: int = 0
+    arch: str = ""
+
+
+@dataclass
+class GpuAlignmentResult:
+    """gpu.rs:25-30."""
+    score: int
+    processing_time_ms: float
+    gpu_device: str
+
+
+@dataclass(frozen=True)
+class Scoring:
+    """Scoring scheme (include/msw.h msw_scoring_t).
+
+    Reference constants: match +2, mismatch -1, linear gap 2
+    (smith_waterman.cl:5-7).  Affine: a gap of length k costs
+    gap_open + k * gap_extend."""
+    match: int = 2
+    mismatch: int = -1
+    gap_open: int = 0
+    gap_extend: int = 2
+    affine: bool = False
+    want_coords: bool = False
+
+    def to_c(self) -> ScoringT:
+        return ScoringT(self.match, self.mismatch, self.gap_open, self.gap_extend,
+                        1 if self.affine else 0, 1 if self.want_coords else 0)
+
+
+LINEAR = Scoring()                                             # config 2
+LINEAR_COORDS = Scoring(want_coords=True)
+AFFINE = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)   # config 3
+
+
+def is_gpu_available() -> bool:
+    """gpu.rs:33-45."""
+    try:
+        n = ctypes.c_int(0)
+        return lib().msw_device_count(ctypes.byref(n)) == 0 and n.value > 0
+    except MswError:
+        return False
+
+
+def get_gpu_devices() -> list:
+    """gpu.rs:48-94 (memory from hipMemGetInfo instead of nvidia-smi)."""
+    n = ctypes.c_int(0)
+    check(lib().msw_device_count(ctypes.byref(n)))
+    out = []
+    for i in range(n.value):
+        info = DeviceInfoT()
+        check(lib().msw_device_info(i, ctypes.byref(info)))
+        out.append(GpuDevice(name=info.name.decode(), memory_gb=info.mem_bytes / 2**30,
+                             max_work_group_size=int(info.max_wg), ordinal=i,
+                             cu_count=int(info.cu_count), arch=info.arch.decode()))
+    return out
+
+
+def _ptr(a) -> int:
+    return a.ctypes.data if a is not None else 0
+
+
+class Context:
+    """One GPU: compute + copy streams and double-buffered pinned staging
+    (replaces the (Context, Queue, Device) singleton of gpu.rs:13-14)."""
+
+    def __init__(self, ordinal: int = 0):
+        self.ordinal = ordinal
+        h = ctypes.c_void_p()
+        check(lib().msw_ctx_create(ordinal, ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise MswError(MSW_E_INVALID, "context is closed")
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            lib().msw_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- batched scoring from host memory --------------------------------------------
+    def align_batch(self, reads: np.ndarray, read_len: np.ndarray, wins: np.ndarray,
+                    win_len: np.ndarray, scoring: Scoring = LINEAR, chunk_pairs: int = 0):
+        """Score a padded SoA batch (uint8 [B, stride] reads / windows, uint16
+        lengths).  Returns (score int32[B], end_i int16[B], end_j int16[B]);
+        the coordinates are None unless ``scoring.want_coords``."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        wins = np.ascontiguousarray(wins, dtype=np.uint8)
+        read_len = np.ascontiguousarray(read_len, dtype=np.uint16)
+        win_len = np.ascontiguousarray(win_len, dtype=np.uint16)
+        B = reads.shape[0]
+        if wins.shape[0] != B or read_len.shape[0] != B or win_len.shape[0] != B:
+            raise MswError(MSW_E_INVALID, "batch arrays disagree on the number of pairs")
+        score = np.zeros(B, np.int32)
+        ei = np.zeros(B, np.int16) if scoring.want_coords else None
+        ej = np.zeros(B, np.int16) if scoring.want_coords else None
+        batch = BatchT(_ptr(reads), _ptr(wins), _ptr(read_len), _ptr(win_len),
+                       reads.shape[1] if reads.ndim == 2 else 0,
+                       wins.shape[1] if wins.ndim == 2 else 0, B)
+        out = OutT(_ptr(score), _ptr(ei), _ptr(ej))
+        sc = scoring.to_c()
+        check(lib().msw_align_batch(self.handle, ctypes.byref(sc), ctypes.byref(batch),
+                                    ctypes.byref(out), chunk_pairs))
+        return score, ei, ej
+
+    # -- HBM-resident batches ----------------------------------------------------------
+    def align_batch_device(self, reads_ptr: int, read_len_ptr: int, wins_ptr: int,
+                           win_len_ptr: int, read_stride: int, win_stride: int, n_pairs: int,
+                           score_ptr: int, max_read_len: int, max_win_len: int,
+                           scoring: Scoring = LINEAR, end_i_ptr: int = 0, end_j_ptr: int = 0,
+                           stream: int = 0) -> None:
+        """Enqueue one scoring pass over device-resident arrays (raw device
+        pointers) on ``stream`` (a hipStream_t handle, 0 = context stream)."""
+        batch = BatchT(reads_ptr, wins_ptr, read_len_ptr, win_len_ptr, read_stride, win_stride,
+                       n_pairs)
+        out = OutT(score_ptr, end_i_ptr, end_j_ptr)
+        sc = scoring.to_c()
+        check(lib().msw_align_batch_device(self.handle, ctypes.byref(sc), ctypes.byref(batch),
+                                           ctypes.byref(out), max_read_len, max_win_len,
+                                           ctypes.c_void_p(stream or None)))
+
+    def synchronize(self) -> None:
+        check(lib().msw_synchronize(self.handle))
+
+    # -- legacy kernel ------------------------------------------------------------------
+    def compat(self, s1: bytes, s2: bytes, wg: int = 0, max_groups: int = 0) -> int:
+        """smith_waterman_align semantics (see gpu_align)."""
+        res = ctypes.c_int32(0)
+        b1 = ctypes.create_string_buffer(s1, len(s1)) if s1 else None
+        b2 = ctypes.create_string_buffer(s2, len(s2)) if s2 else None
+        check(lib().msw_align_compat(self.handle, b1, len(s1), b2, len(s2), wg, max_groups,
+                                     ctypes.byref(res)))
+        return int(res.value)
+
+
+_contexts: dict = {}
+_ctx_lock = threading.Lock()
+
+
+def get_context(device=0) -> Context:
+    """Process-wide context per GPU (gpu.rs:97-109 get_opencl_context)."""
+    ordinal = device.ordinal if isinstance(device, GpuDevice) else int(device)
+    with _ctx_lock:
+        ctx = _contexts.get(ordinal)
+        if ctx is None:
+            ctx = _contexts[ordinal] = Context(ordinal)
+        return ctx
+
+
+def gpu_align(seq1: str, seq2: str, device: GpuDevice) -> int:
+    """aligner.rs:410-532: the score of the kernel the reference launches
+    (smith_waterman_align), with its host geometry W = min(max_wg, 1024),
+    G = min(ceil(L/W), 1e6); L == 0 -> 0; oversize -> MswError."""
+    b1 = seq1.encode() if isinstance(seq1, str) else bytes(seq1)
+    b2 = seq2.encode() if isinstance(seq2, str) else bytes(seq2)
+    wg = min(int(device.max_work_group_size), GPU_WORK_GROUP_SIZE)
+    return get_context(device).compat(b1, b2, wg, GPU_MAX_WORK_GROUPS)
+
+
+def gpu_align_chunk_self(chunk: str, device: GpuDevice) -> int:
+    """aligner.rs:365-373: chunks under 1000 bases score 0, else self-align."""
+    if len(chunk) < 1000:
+        return 0
+    return gpu_align(chunk, chunk, device)
+
+
+def get_chunk_size_reads() -> int:
+    """aligner.rs:9-15: GPU_CHUNK_SIZE_READS is mandatory."""
+    v = os.environ.get("GPU_CHUNK_SIZE_READS")
+    if v is None:
+        raise MswError(MSW_E_INVALID, "GPU_CHUNK_SIZE_READS not set in .env file")
+    try:
+        n = int(v)
+        if n < 0:
+            raise ValueError(v)
+        return n
+    except ValueError as e:
+        raise MswError(MSW_E_INVALID, f"Invalid GPU_CHUNK_SIZE_READS value '{v}': {e}") from None
+
+
+def pack_batch(reads: Sequence[bytes], wins: Sequence[bytes], read_stride: Optional[int] = None,
+               win_stride: Optional[int] = None):
+    """Lists of byte strings -> padded SoA arrays (reads, read_len, wins, win_len)."""
+    B = len(reads)
+    if len(wins) != B:
+        raise MswError(MSW_E_INVALID, "reads and windows differ in count")
+    rl = np.array([len(r) for r in reads], np.uint16)
+    wl = np.array([len(w) for w in wins], np.uint16)
+    rs = read_stride or max(16, (int(rl.max()) if B else 0) + 15) // 16 * 16
+    ws = win_stride or max(16, (int(wl.max()) if B else 0) + 15) // 16 * 16
+    R = np.zeros((B, rs), np.uint8)
+    W = np.zeros((B, ws), np.uint8)
+    for i, (r, w) in enumerate(zip(reads, wins)):
+        R[i, :len(r)] = np.frombuffer(bytes(r), np.uint8)
+        W[i, :len(w)] = np.frombuffer(bytes(w), np.uint8)
+    return R, rl, W, wl

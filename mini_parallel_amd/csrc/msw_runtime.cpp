@@ -1,0 +1,596 @@
+// msw_runtime.cpp -- device runtime and C ABI (include/msw.h) for the
+// MI355X-native batched Smith-Waterman scorer.
+//
+// Replaces (smith_waterman/src/):
+//   gpu.rs:33-132        OpenCL discovery + Mutex'd context singleton
+//                        -> msw_device_count/info, one msw_ctx per device
+//   aligner.rs:410-532   gpu_align: per-call JIT, buffer build, blocking finish
+//                        -> msw_align_compat (kernels compiled ahead of time)
+//   aligner.rs:269-289   per-chunk concat + gpu_align loop
+//                        -> msw_align_batch: pinned double-buffered staging, H2D
+//                           on a copy stream overlapped with the kernels
+//   system_info.rs:236-243  80 % memory cap -> hipMemGetInfo
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/msw.h"
+#include "msw_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(MSW_E_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                        __FILE__, __LINE__);                                                   \
+    } while (0)
+
+inline uint32_t dup16(uint32_t v) { return (v & 0xFFFFu) | ((v & 0xFFFFu) << 16); }
+
+// Validated kernel constants for one scoring scheme.
+struct Scheme {
+    bool affine, coords;
+    uint32_t match2, delta2, gap2, open_ext2, code_shift;
+    int32_t match;
+};
+
+int make_scheme(const msw_scoring_t* sc, Scheme* s) {
+    if (!sc) return fail(MSW_E_INVALID, "scoring is NULL");
+    if (sc->match < 1 || sc->match > 64)
+        return fail(MSW_E_RANGE, "match=%d outside [1, 64]", sc->match);
+    if (sc->mismatch > 0 || sc->match - sc->mismatch > 64)
+        return fail(MSW_E_RANGE, "mismatch=%d outside [match-64, 0]", sc->mismatch);
+    if (sc->gap_extend < 0 || sc->gap_open < 0)
+        return fail(MSW_E_RANGE, "negative gap penalty (open=%d extend=%d)", sc->gap_open,
+                    sc->gap_extend);
+    if (sc->gap_extend > 30000 || sc->gap_open > 30000)
+        return fail(MSW_E_RANGE, "gap penalty too large");
+    s->affine = sc->affine != 0;
+    s->coords = sc->want_coords != 0;
+    s->match = sc->match;
+    const uint32_t delta = (uint32_t)(sc->match - sc->mismatch);
+    uint32_t shift = 0;
+    while ((1u << shift) < delta) ++shift;
+    s->code_shift = shift;
+    s->match2 = dup16((uint32_t)sc->match);
+    s->delta2 = dup16(delta);
+    s->gap2 = dup16((uint32_t)sc->gap_extend);
+    s->open_ext2 = dup16((uint32_t)(sc->gap_open + sc->gap_extend));
+    return MSW_OK;
+}
+
+// Score bound: every cell value (and H + match) must stay a finite,
+// non-negative f16 bit pattern (< 0x7C00) for v_pk_maximum3_f16.
+int check_bounds(const Scheme& s, uint32_t max_m, uint32_t max_n) {
+    if (max_m > (uint32_t)msw::kMaxReadLen)
+        return fail(MSW_E_RANGE, "read length %u > %d", max_m, msw::kMaxReadLen);
+    if (max_n > (uint32_t)msw::kMaxWinLen)
+        return fail(MSW_E_RANGE, "window length %u > %d", max_n, msw::kMaxWinLen);
+    const uint64_t bound = (uint64_t)s.match * (std::min(max_m, max_n) + 1u);
+    if (bound >= 0x7C00u)
+        return fail(MSW_E_RANGE, "match*(len+1)=%llu exceeds the 16-bit score range",
+                    (unsigned long long)bound);
+    return MSW_OK;
+}
+
+msw::SwParams base_params(const Scheme& s) {
+    msw::SwParams p;
+    memset(&p, 0, sizeof(p));
+    p.code_shift = s.code_shift;
+    p.match2 = s.match2;
+    p.delta2 = s.delta2;
+    p.gap2 = s.gap2;
+    p.open_ext2 = s.open_ext2;
+    return p;
+}
+
+// Device + pinned buffers for one in-flight chunk.
+struct Slot {
+    size_t cap_pairs = 0, cap_read = 0, cap_win = 0;
+    uint8_t *d_reads = nullptr, *d_wins = nullptr;
+    uint16_t *d_rlen = nullptr, *d_wlen = nullptr;
+    uint32_t* d_order = nullptr;
+    int32_t* d_score = nullptr;
+    int16_t *d_ei = nullptr, *d_ej = nullptr;
+    uint8_t *h_reads = nullptr, *h_wins = nullptr;
+    uint16_t *h_rlen = nullptr, *h_wlen = nullptr;
+    uint32_t* h_order = nullptr;
+    int32_t* h_score = nullptr;
+    int16_t *h_ei = nullptr, *h_ej = nullptr;
+    hipEvent_t uploaded = nullptr, done = nullptr;
+    bool busy = false;
+    // Pending readback bookkeeping.
+    uint64_t first = 0, count = 0;
+    msw_out_t out{};
+};
+
+void free_slot(Slot& s) {
+    hipFree(s.d_reads); hipFree(s.d_wins); hipFree(s.d_rlen); hipFree(s.d_wlen);
+    hipFree(s.d_order); hipFree(s.d_score); hipFree(s.d_ei); hipFree(s.d_ej);
+    hipHostFree(s.h_reads); hipHostFree(s.h_wins); hipHostFree(s.h_rlen); hipHostFree(s.h_wlen);
+    hipHostFree(s.h_order); hipHostFree(s.h_score); hipHostFree(s.h_ei); hipHostFree(s.h_ej);
+    s = Slot{};
+}
+
+}  // namespace
+
+struct msw_ctx {
+    int device = 0;
+    hipStream_t compute = nullptr, copy = nullptr;
+    Slot slots[2];
+    hipEvent_t slot_events[4] = {};
+    uint64_t next_ticket = 1, done_ticket = 0;
+    // compat buffers
+    uint8_t *c_s1 = nullptr, *c_s2 = nullptr;
+    int32_t* c_res = nullptr;
+    size_t c_cap = 0;
+};
+
+namespace {
+
+int set_device(msw_ctx* ctx) {
+    HIP_TRY(hipSetDevice(ctx->device));
+    return MSW_OK;
+}
+
+template <typename T>
+int grow_dev(T** p, size_t n) {
+    hipFree(*p);
+    *p = nullptr;
+    if (n == 0) return MSW_OK;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e != hipSuccess) return fail(MSW_E_NOMEM, "hipMalloc(%zu B): %s", n * sizeof(T), hipGetErrorString(e));
+    return MSW_OK;
+}
+template <typename T>
+int grow_host(T** p, size_t n) {
+    hipHostFree(*p);
+    *p = nullptr;
+    if (n == 0) return MSW_OK;
+    hipError_t e = hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault);
+    if (e != hipSuccess) return fail(MSW_E_NOMEM, "hipHostMalloc(%zu B): %s", n * sizeof(T), hipGetErrorString(e));
+    return MSW_OK;
+}
+
+int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
+    int rc;
+    if (!s.uploaded) {
+        HIP_TRY(hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    }
+    if (pairs > s.cap_pairs) {
+        if ((rc = grow_dev(&s.d_rlen, pairs)) || (rc = grow_dev(&s.d_wlen, pairs)) ||
+            (rc = grow_dev(&s.d_order, pairs)) || (rc = grow_dev(&s.d_score, pairs)) ||
+            (rc = grow_dev(&s.d_ei, pairs)) || (rc = grow_dev(&s.d_ej, pairs)) ||
+            (rc = grow_host(&s.h_rlen, pairs)) || (rc = grow_host(&s.h_wlen, pairs)) ||
+            (rc = grow_host(&s.h_order, pairs)) || (rc = grow_host(&s.h_score, pairs)) ||
+            (rc = grow_host(&s.h_ei, pairs)) || (rc = grow_host(&s.h_ej, pairs)))
+            return rc;
+        s.cap_pairs = pairs;
+    }
+    if (read_bytes > s.cap_read) {
+        if ((rc = grow_dev(&s.d_reads, read_bytes)) || (rc = grow_host(&s.h_reads, read_bytes))) return rc;
+        s.cap_read = read_bytes;
+    }
+    if (win_bytes > s.cap_win) {
+        if ((rc = grow_dev(&s.d_wins, win_bytes)) || (rc = grow_host(&s.h_wins, win_bytes))) return rc;
+        s.cap_win = win_bytes;
+    }
+    return MSW_OK;
+}
+
+uint64_t default_chunk() {
+    // aligner.rs:9-15 reads GPU_CHUNK_SIZE_READS (mandatory there); here it is
+    // optional and defaults to a size that fills the GPU.
+    const char* v = getenv("GPU_CHUNK_SIZE_READS");
+    if (v && *v) {
+        char* end = nullptr;
+        unsigned long long n = strtoull(v, &end, 10);
+        if (end && *end == '\0' && n > 0) return n;
+    }
+    return 65536;
+}
+
+// Buckets of one chunk: pairs grouped by rows-per-lane (read length / 16), and
+// inside a bucket by window length, so every wave runs with tight bounds.
+struct Bucket {
+    uint32_t begin, count, max_m, max_n;
+};
+
+void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32_t* order,
+                  std::vector<Bucket>& buckets) {
+    buckets.clear();
+    // key = KR (1..16) * 256 + ceil(n / 16) (<= 256): counting sort.
+    constexpr int kKeys = 17 * 257;
+    std::vector<uint32_t> hist(kKeys + 1, 0);
+    auto key_of = [&](uint64_t i) {
+        const int kr = msw::rows_per_lane(rlen[i]);
+        const int nb = (wlen[i] + 15) / 16;
+        return kr * 257 + nb;
+    };
+    for (uint64_t i = 0; i < n; ++i) hist[key_of(i) + 1]++;
+    for (int k = 0; k < kKeys; ++k) hist[k + 1] += hist[k];
+    std::vector<uint32_t> pos(hist.begin(), hist.end() - 1);
+    for (uint64_t i = 0; i < n; ++i) order[pos[key_of(i)]++] = (uint32_t)i;
+    // One bucket per KR value; the window bound is the bucket's max.
+    for (int kr = 1; kr <= 16; ++kr) {
+        const uint32_t b = hist[kr * 257], e = hist[kr * 257 + 257];
+        if (e <= b) continue;
+        uint32_t mm = 0, mn = 0;
+        for (uint32_t s = b; s < e; ++s) {
+            mm = std::max<uint32_t>(mm, rlen[order[s]]);
+            mn = std::max<uint32_t>(mn, wlen[order[s]]);
+        }
+        buckets.push_back({b, e - b, mm, mn});
+    }
+}
+
+int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const std::vector<Bucket>& buckets,
+                   bool use_order, uint32_t read_stride, uint32_t win_stride) {
+    for (const Bucket& b : buckets) {
+        msw::SwParams p = base_params(sch);
+        p.reads = s.d_reads;
+        p.wins = s.d_wins;
+        p.read_len = s.d_rlen;
+        p.win_len = s.d_wlen;
+        p.order = use_order ? s.d_order + b.begin : nullptr;
+        p.score = s.d_score;
+        p.end_i = sch.coords ? s.d_ei : nullptr;
+        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.read_stride = read_stride;
+        p.win_stride = win_stride;
+        p.n_slots = b.count;
+        p.lds_stride = msw::stream_stride(b.max_n);
+        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, ctx->compute));
+    }
+    (void)n;
+    return MSW_OK;
+}
+
+// Copy finished results of a slot into the caller's arrays.
+void drain_slot(Slot& s) {
+    if (!s.busy) return;
+    hipEventSynchronize(s.done);
+    memcpy(s.out.score + s.first, s.h_score, s.count * sizeof(int32_t));
+    if (s.out.end_i) memcpy(s.out.end_i + s.first, s.h_ei, s.count * sizeof(int16_t));
+    if (s.out.end_j) memcpy(s.out.end_j + s.first, s.h_ej, s.count * sizeof(int16_t));
+    s.busy = false;
+}
+
+int validate_batch(const msw_batch_t* b, const msw_out_t* out, const Scheme& sch) {
+    if (!b || !out) return fail(MSW_E_INVALID, "batch/out is NULL");
+    if (b->n_pairs == 0) return MSW_OK;
+    if (!b->reads || !b->wins || !b->read_len || !b->win_len || !out->score)
+        return fail(MSW_E_INVALID, "NULL array in batch/out");
+    if (sch.coords && (!out->end_i || !out->end_j))
+        return fail(MSW_E_INVALID, "want_coords set but end_i/end_j is NULL");
+    if (b->n_pairs > 0xFFFFFFFFull) return fail(MSW_E_RANGE, "n_pairs > 2^32-1");
+    return MSW_OK;
+}
+
+int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* b, msw_out_t* out,
+              uint64_t chunk_pairs, bool sync) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    Scheme sch;
+    int rc;
+    if ((rc = make_scheme(sc, &sch))) return rc;
+    if ((rc = validate_batch(b, out, sch))) return rc;
+    if ((rc = set_device(ctx))) return rc;
+    const uint64_t n = b->n_pairs;
+    if (n == 0) return MSW_OK;
+    // Host-side range checks over the whole batch first: fail before any launch.
+    uint32_t gm = 0, gn = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        gm = std::max<uint32_t>(gm, b->read_len[i]);
+        gn = std::max<uint32_t>(gn, b->win_len[i]);
+    }
+    if (gm > b->read_stride || gn > b->win_stride)
+        return fail(MSW_E_INVALID, "length exceeds stride (max read %u / stride %u, max window %u / stride %u)",
+                    gm, b->read_stride, gn, b->win_stride);
+    if ((rc = check_bounds(sch, gm, gn))) return rc;
+
+    const uint64_t chunk = chunk_pairs ? chunk_pairs : default_chunk();
+    std::vector<Bucket> buckets;
+    uint64_t c = 0;
+    for (uint64_t first = 0; first < n; first += chunk, ++c) {
+        const uint64_t cnt = std::min(chunk, n - first);
+        Slot& s = ctx->slots[c & 1];
+        drain_slot(s);  // the slot's previous chunk must be out before reuse
+        if ((rc = ensure_slot(s, cnt, cnt * b->read_stride, cnt * b->win_stride))) return rc;
+        // Stage the chunk in pinned memory.  (FASTQ callers fill these slabs
+        // directly; see msw_fastq.cpp.)
+        memcpy(s.h_reads, b->reads + first * b->read_stride, cnt * b->read_stride);
+        memcpy(s.h_wins, b->wins + first * b->win_stride, cnt * b->win_stride);
+        memcpy(s.h_rlen, b->read_len + first, cnt * sizeof(uint16_t));
+        memcpy(s.h_wlen, b->win_len + first, cnt * sizeof(uint16_t));
+        bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets);
+        bool uniform = buckets.size() == 1;
+        if (uniform) {
+            // One read-length bucket: order only matters if windows vary a lot.
+            uint32_t mn = 0xFFFF, mx = 0;
+            for (uint64_t i = 0; i < cnt; ++i) { mn = std::min<uint32_t>(mn, s.h_wlen[i]); mx = std::max<uint32_t>(mx, s.h_wlen[i]); }
+            uniform = (mx - mn) < 16;
+        }
+        // H2D on the copy stream, kernels on the compute stream.
+        HIP_TRY(hipMemcpyAsync(s.d_reads, s.h_reads, cnt * b->read_stride, hipMemcpyHostToDevice, ctx->copy));
+        HIP_TRY(hipMemcpyAsync(s.d_wins, s.h_wins, cnt * b->win_stride, hipMemcpyHostToDevice, ctx->copy));
+        HIP_TRY(hipMemcpyAsync(s.d_rlen, s.h_rlen, cnt * sizeof(uint16_t), hipMemcpyHostToDevice, ctx->copy));
+        HIP_TRY(hipMemcpyAsync(s.d_wlen, s.h_wlen, cnt * sizeof(uint16_t), hipMemcpyHostToDevice, ctx->copy));
+        if (!uniform)
+            HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->copy));
+        HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
+        HIP_TRY(hipStreamWaitEvent(ctx->compute, s.uploaded, 0));
+        if (uniform) {
+            buckets.resize(1);
+            buckets[0].begin = 0;
+        }
+        if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, b->read_stride, b->win_stride))) return rc;
+        HIP_TRY(hipMemcpyAsync(s.h_score, s.d_score, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->compute));
+        if (sch.coords) {
+            HIP_TRY(hipMemcpyAsync(s.h_ei, s.d_ei, cnt * sizeof(int16_t), hipMemcpyDeviceToHost, ctx->compute));
+            HIP_TRY(hipMemcpyAsync(s.h_ej, s.d_ej, cnt * sizeof(int16_t), hipMemcpyDeviceToHost, ctx->compute));
+        }
+        HIP_TRY(hipEventRecord(s.done, ctx->compute));
+        s.busy = true;
+        s.first = first;
+        s.count = cnt;
+        s.out = *out;
+        if (!sch.coords) { s.out.end_i = nullptr; s.out.end_j = nullptr; }
+    }
+    if (sync) {
+        drain_slot(ctx->slots[0]);
+        drain_slot(ctx->slots[1]);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
+    }
+    return MSW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* msw_last_error(void) { return g_last_error.c_str(); }
+
+const char* msw_version(void) { return "msw 0.1.0 (gfx950, HIP)"; }
+
+int msw_device_count(int* n) {
+    if (!n) return fail(MSW_E_INVALID, "n is NULL");
+    *n = 0;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess || c == 0) return fail(MSW_E_NODEVICE, "no GPU: %s", hipGetErrorString(e));
+    *n = c;
+    return MSW_OK;
+}
+
+int msw_device_info(int ordinal, msw_device_info_t* out) {
+    if (!out) return fail(MSW_E_INVALID, "out is NULL");
+    int n = 0;
+    int rc = msw_device_count(&n);
+    if (rc) return rc;
+    if (ordinal < 0 || ordinal >= n) return fail(MSW_E_INVALID, "device %d out of range [0,%d)", ordinal, n);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, ordinal));
+    memset(out, 0, sizeof(*out));
+    snprintf(out->name, sizeof(out->name), "%s", prop.name);
+    snprintf(out->arch, sizeof(out->arch), "%s", prop.gcnArchName);
+    out->mem_bytes = prop.totalGlobalMem;
+    out->max_wg = (uint32_t)prop.maxThreadsPerBlock;
+    out->cu_count = (uint32_t)prop.multiProcessorCount;
+    int cur = 0;
+    hipGetDevice(&cur);
+    if (hipSetDevice(ordinal) == hipSuccess) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) out->mem_free_bytes = fr;
+        hipSetDevice(cur);
+    }
+    return MSW_OK;
+}
+
+int msw_ctx_create(int ordinal, msw_ctx** out) {
+    if (!out) return fail(MSW_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    int rc = msw_device_count(&n);
+    if (rc) return rc;
+    if (ordinal < 0 || ordinal >= n) return fail(MSW_E_INVALID, "device %d out of range [0,%d)", ordinal, n);
+    msw_ctx* c = new msw_ctx();
+    c->device = ordinal;
+    hipError_t e = hipSetDevice(ordinal);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(MSW_E_DEVICE, "context creation on device %d failed: %s", ordinal, hipGetErrorString(e));
+    }
+    *out = c;
+    return MSW_OK;
+}
+
+void msw_ctx_destroy(msw_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->compute) hipStreamSynchronize(ctx->compute);
+    if (ctx->copy) hipStreamSynchronize(ctx->copy);
+    for (Slot& s : ctx->slots) {
+        if (s.uploaded) hipEventDestroy(s.uploaded);
+        if (s.done) hipEventDestroy(s.done);
+        free_slot(s);
+    }
+    hipFree(ctx->c_s1);
+    hipFree(ctx->c_s2);
+    hipFree(ctx->c_res);
+    if (ctx->compute) hipStreamDestroy(ctx->compute);
+    if (ctx->copy) hipStreamDestroy(ctx->copy);
+    delete ctx;
+}
+
+int msw_align_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch, msw_out_t* out,
+                    uint64_t chunk_pairs) {
+    return run_batch(ctx, sc, batch, out, chunk_pairs, true);
+}
+
+int msw_align_batch_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch, msw_out_t* out,
+                          uint64_t chunk_pairs, uint64_t* ticket) {
+    if (!ticket) return fail(MSW_E_INVALID, "ticket is NULL");
+    int rc = run_batch(ctx, sc, batch, out, chunk_pairs, false);
+    if (rc) return rc;
+    *ticket = ctx->next_ticket++;
+    return MSW_OK;
+}
+
+int msw_wait(msw_ctx* ctx, uint64_t ticket) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    if (ticket == 0 || ticket >= ctx->next_ticket) return fail(MSW_E_INVALID, "unknown ticket %llu", (unsigned long long)ticket);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    // Tickets complete in order: draining both slots completes every earlier ticket.
+    drain_slot(ctx->slots[0]);
+    drain_slot(ctx->slots[1]);
+    ctx->done_ticket = ctx->next_ticket - 1;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
+    return MSW_OK;
+}
+
+int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* b, msw_out_t* out,
+                           uint32_t max_read_len, uint32_t max_win_len, void* stream) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    Scheme sch;
+    int rc;
+    if ((rc = make_scheme(sc, &sch))) return rc;
+    if ((rc = validate_batch(b, out, sch))) return rc;
+    if (b->n_pairs == 0) return MSW_OK;
+    if ((rc = check_bounds(sch, max_read_len, max_win_len))) return rc;
+    if (max_read_len > b->read_stride || max_win_len > b->win_stride)
+        return fail(MSW_E_INVALID, "max length exceeds stride");
+    if ((rc = set_device(ctx))) return rc;
+    msw::SwParams p = base_params(sch);
+    p.reads = b->reads;
+    p.wins = b->wins;
+    p.read_len = b->read_len;
+    p.win_len = b->win_len;
+    p.order = nullptr;
+    p.score = out->score;
+    p.end_i = sch.coords ? out->end_i : nullptr;
+    p.end_j = sch.coords ? out->end_j : nullptr;
+    p.read_stride = b->read_stride;
+    p.win_stride = b->win_stride;
+    p.n_slots = (uint32_t)b->n_pairs;
+    p.lds_stride = msw::stream_stride(max_win_len);
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, st));
+    return MSW_OK;
+}
+
+int msw_align_compat(msw_ctx* ctx, const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2, uint32_t wg,
+                     uint32_t max_groups, int32_t* score) {
+    if (!ctx || !score) return fail(MSW_E_INVALID, "ctx/score is NULL");
+    *score = 0;
+    const size_t L = std::min(n1, n2);
+    if (L == 0) return MSW_OK;                                 // aligner.rs:414-416
+    if (!s1 || !s2) return fail(MSW_E_INVALID, "NULL sequence");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, ctx->device));
+    const uint32_t W = wg ? wg : std::min<uint32_t>((uint32_t)prop.maxThreadsPerBlock, 1024u);  // aligner.rs:422
+    const uint64_t G = std::min<uint64_t>((L + W - 1) / W, max_groups ? max_groups : 1000000u);  // :423-424
+    // aligner.rs:436-456: min(1,000,000 * 1024 work items, 80 % of memory / 3).
+    size_t fr = 0, tot = 0;
+    HIP_TRY(hipMemGetInfo(&fr, &tot));
+    const uint64_t cap = std::min<uint64_t>(1024000000ull, (uint64_t)(tot * 0.8) / 3);
+    if (L > cap)
+        return fail(MSW_E_RANGE, "Sequence too large (%zu bytes), max allowed: %llu bytes (%llu MB)", L,
+                    (unsigned long long)cap, (unsigned long long)(cap / (1024 * 1024)));
+    if (L > ctx->c_cap) {
+        if ((rc = grow_dev(&ctx->c_s1, L)) || (rc = grow_dev(&ctx->c_s2, L))) return rc;
+        ctx->c_cap = L;
+    }
+    if (!ctx->c_res && (rc = grow_dev(&ctx->c_res, 1))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->c_s1, s1, L, hipMemcpyHostToDevice, ctx->compute));
+    HIP_TRY(hipMemcpyAsync(ctx->c_s2, s2, L, hipMemcpyHostToDevice, ctx->compute));
+    HIP_TRY(hipMemsetAsync(ctx->c_res, 0, sizeof(int32_t), ctx->compute));
+    HIP_TRY(msw::launch_compat(ctx->c_s1, ctx->c_s2, ctx->c_res, L, W, G, ctx->compute));
+    HIP_TRY(hipMemcpyAsync(score, ctx->c_res, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->compute));
+    HIP_TRY(hipStreamSynchronize(ctx->compute));
+    return MSW_OK;
+}
+
+void* msw_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        fail(MSW_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
+        return nullptr;
+    }
+    return p;
+}
+
+void msw_host_free(void* p) {
+    if (p) hipHostFree(p);
+}
+
+void* msw_dev_alloc(msw_ctx* ctx, size_t bytes) {
+    if (!ctx || set_device(ctx)) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        fail(MSW_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+        return nullptr;
+    }
+    return p;
+}
+
+void msw_dev_free(msw_ctx* ctx, void* p) {
+    if (ctx) hipSetDevice(ctx->device);
+    if (p) hipFree(p);
+}
+
+int msw_memcpy_h2d(msw_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return MSW_OK;
+}
+
+int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return MSW_OK;
+}
+
+int msw_synchronize(msw_ctx* ctx) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->compute));
+    HIP_TRY(hipStreamSynchronize(ctx->copy));
+    HIP_TRY(hipGetLastError());
+    return MSW_OK;
+}
+
+}  // extern "C"

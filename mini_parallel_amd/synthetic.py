@@ -1,0 +1,107 @@
+"""Seeded synthetic short-read pairs (BASELINE.json configs).
+
+A uniform i.i.d. ACGT genome; each read copies genome[p:p+m] with 1 %
+substitutions, 0.1 % indels and 0.05 % 'N'; its window is the length-n
+stretch of genome centred on the read; 10 % of reads are unrelated random
+sequence (they exercise the zero floor).  Seed 1000 + k for config k.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+
+
+@dataclass
+class PairBatch:
+    reads: np.ndarray      # uint8 [B, read_stride]
+    read_len: np.ndarray   # uint16 [B]
+    wins: np.ndarray       # uint8 [B, win_stride]
+    win_len: np.ndarray    # uint16 [B]
+    pos: np.ndarray        # int64 [B] genome offset of the window (-1: unrelated read)
+
+    @property
+    def n_pairs(self) -> int:
+        return int(self.reads.shape[0])
+
+    @property
+    def cells(self) -> int:
+        return int(np.sum(self.read_len.astype(np.int64) * self.win_len.astype(np.int64)))
+
+    def slice(self, a: int, b: int) -> "PairBatch":
+        return PairBatch(self.reads[a:b], self.read_len[a:b], self.wins[a:b], self.win_len[a:b],
+                         self.pos[a:b])
+
+
+def genome(n_bases: int, rng: np.random.Generator) -> np.ndarray:
+    return ACGT[rng.integers(0, 4, n_bases, dtype=np.uint8)]
+
+
+def make_pairs(n_pairs: int, read_len, win_factor: float = 2.0, seed: int = 1002,
+               genome_bases: int = 1 << 22, unrelated: float = 0.10, read_stride: int = 0,
+               win_stride: int = 0, sub: float = 0.01, indel: float = 0.001,
+               nrate: float = 0.0005) -> PairBatch:
+    """``read_len`` is an int (fixed length) or an (lo, hi) range for mixed
+    lengths (config 5); window length = round(win_factor * read length).
+    Vectorised over pairs; only reads that draw an indel take a Python loop."""
+    rng = np.random.default_rng(seed)
+    g = genome(genome_bases, rng)
+    if isinstance(read_len, (tuple, list)):
+        lens = rng.integers(read_len[0], read_len[1] + 1, n_pairs)
+    else:
+        lens = np.full(n_pairs, int(read_len), np.int64)
+    wlens = np.round(lens * win_factor).astype(np.int64)
+    max_m = int(lens.max()) if n_pairs else 0
+    max_n = int(wlens.max()) if n_pairs else 0
+    rs = read_stride or max(16, (max_m + 15) // 16 * 16)
+    ws = win_stride or max(16, (max_n + 15) // 16 * 16)
+    assert rs >= max_m and ws >= max_n, "stride smaller than the longest sequence"
+    pos = rng.integers(0, genome_bases - max(max_n, 1), n_pairs)
+    cols_w = np.arange(ws)
+    wins = g[np.minimum(pos[:, None] + cols_w[None, :], genome_bases - 1)]
+    wins[cols_w[None, :] >= wlens[:, None]] = 0
+    # read = genome[off : off + m], centred in the window
+    off = pos + (wlens - lens) // 2
+    cols_r = np.arange(rs)
+    reads = g[np.minimum(off[:, None] + cols_r[None, :], genome_bases - 1)]
+    valid = cols_r[None, :] < lens[:, None]
+    subs = (rng.random(reads.shape) < sub) & valid
+    idx = np.searchsorted(ACGT, reads[subs])
+    reads[subs] = ACGT[(idx + rng.integers(1, 4, idx.shape[0])) % 4]
+    reads[(rng.random(reads.shape) < nrate) & valid] = ord("N")
+    unrel = rng.random(n_pairs) < unrelated
+    reads[unrel] = ACGT[rng.integers(0, 4, (int(unrel.sum()), rs), dtype=np.uint8)]
+    reads[~valid] = 0
+    rl = lens.copy()
+    n_indel = rng.binomial(lens, indel)
+    for k in np.nonzero((n_indel > 0) & ~unrel)[0]:
+        r = reads[k, :rl[k]]
+        for _ in range(int(n_indel[k])):
+            at = int(rng.integers(0, max(1, r.shape[0])))
+            if rng.random() < 0.5 and r.shape[0] > 1:
+                r = np.delete(r, at)
+            else:
+                r = np.insert(r, at, ACGT[int(rng.integers(0, 4))])
+        r = r[:rs]
+        reads[k, :] = 0
+        reads[k, :r.shape[0]] = r
+        rl[k] = r.shape[0]
+    pos = np.where(unrel, -1, pos)
+    return PairBatch(np.ascontiguousarray(reads), rl.astype(np.uint16),
+                     np.ascontiguousarray(wins), wlens.astype(np.uint16), pos)
+
+
+def config_batch(k: int, n_pairs: int = 0, seed_offset: int = 0) -> PairBatch:
+    """Batches for BASELINE.json configs (k = 1..5); n_pairs overrides the size."""
+    seed = 1000 + k + seed_offset
+    if k == 1:
+        return make_pairs(n_pairs or 1, 32, win_factor=1.0, seed=seed, unrelated=0.0)
+    if k in (2, 3, 4):
+        default = {2: 10_000, 3: 1_000_000, 4: 1_000_000}[k]
+        return make_pairs(n_pairs or default, 150, 2.0, seed=seed, read_stride=160, win_stride=304)
+    if k == 5:
+        return make_pairs(n_pairs or 100_000, (75, 250), 2.0, seed=seed, read_stride=256,
+                          win_stride=512)
+    raise ValueError(f"unknown config {k}")

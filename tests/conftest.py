@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle_lib
+    oracle_lib.build()
+    return oracle_lib
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    """One context for the whole GPU session (one process on the card)."""
+    from mini_parallel_amd import Context, is_gpu_available
+    if not is_gpu_available():
+        pytest.fail("-m gpu tests need a GPU and the built libmsw.so (no CPU fallback)")
+    ctx = Context(0)
+    yield ctx
+    ctx.close()

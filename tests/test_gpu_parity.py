@@ -1,0 +1,228 @@
+"""GPU parity: the HIP kernels, called through the C ABI, must be bit-exact
+against the oracle (scores and best-cell coordinates).  Run with -m gpu."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import mini_parallel_amd as mpa
+from mini_parallel_amd import Scoring
+from mini_parallel_amd.synthetic import config_batch, make_pairs
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def oracle_run(oracle, b, sc: Scoring):
+    return oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, match=sc.match,
+                           mismatch=sc.mismatch, gap_open=sc.gap_open, gap_extend=sc.gap_extend,
+                           affine=sc.affine, threads=THREADS)
+
+
+def gpu_run(ctx, b, sc: Scoring, chunk=0):
+    return ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc, chunk_pairs=chunk)
+
+
+def assert_same(got, want, coords: bool):
+    s, i, j = got
+    ws, wi, wj = want
+    bad = np.nonzero(s != ws)[0]
+    assert bad.size == 0, f"{bad.size} score mismatches, first at {bad[:5]}: gpu {s[bad[:5]]} oracle {ws[bad[:5]]}"
+    if coords:
+        bad = np.nonzero((i != wi) | (j != wj))[0]
+        assert bad.size == 0, (f"{bad.size} coordinate mismatches, first {bad[:5]}: gpu "
+                               f"{list(zip(i[bad[:5]], j[bad[:5]]))} oracle {list(zip(wi[bad[:5]], wj[bad[:5]]))}")
+
+
+class B:  # minimal batch holder
+    def __init__(self, reads, read_len, wins, win_len):
+        self.reads, self.read_len, self.wins, self.win_len = reads, read_len, wins, win_len
+
+
+def test_device_visible(gpu_ctx):
+    devs = mpa.get_gpu_devices()
+    assert devs and devs[0].arch.startswith("gfx950"), devs
+
+
+@pytest.mark.parametrize("section,sc", [
+    ("linear_2_-1_2", Scoring(want_coords=True)),
+    ("affine_2_-1_o3_e1", Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)),
+])
+def test_kat(gpu_ctx, section, sc):
+    kats = json.load(open(os.path.join(GOLDEN, "kat.json")))[section]
+    R, rl, W, wl = mpa.pack_batch([k["read"].encode() for k in kats], [k["window"].encode() for k in kats])
+    s, i, j = gpu_ctx.align_batch(R, rl, W, wl, sc)
+    for k, a, b, c in zip(kats, s, i, j):
+        assert (int(a), int(b), int(c)) == (k["score"], k["end_i"], k["end_j"]), k
+
+
+@pytest.mark.parametrize("name", ["linear_150x300.npz", "affine_150x300.npz", "mixed_linear.npz"])
+@pytest.mark.parametrize("coords", [False, True])
+def test_golden(gpu_ctx, name, coords):
+    z = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    sc = Scoring(match=meta["match"], mismatch=meta["mismatch"], gap_open=meta.get("gap_open", 0),
+                 gap_extend=meta["gap_extend"], affine=meta["affine"], want_coords=coords)
+    got = gpu_ctx.align_batch(z["reads"], z["read_len"], z["wins"], z["win_len"], sc)
+    assert_same(got, (z["score"], z["end_i"], z["end_j"]), coords)
+
+
+def test_config2_linear_score_only(gpu_ctx, oracle):
+    """BASELINE config 2 at full size: 10k x (150 bp, 300 bp), linear, score-only."""
+    b = config_batch(2)
+    sc = Scoring()
+    assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), False)
+
+
+def test_config3_affine_coords_sample(gpu_ctx, oracle):
+    """Config 3 shape (affine + best cell), chunked through the pinned pipeline."""
+    b = config_batch(3, n_pairs=40_000)
+    sc = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)
+    assert_same(gpu_run(gpu_ctx, b, sc, chunk=9_000), oracle_run(oracle, b, sc), True)
+
+
+def test_config5_mixed_lengths(gpu_ctx, oracle):
+    """Config 5 shape: 75-250 bp reads, window 2m, length-bucketed dispatch."""
+    b = config_batch(5, n_pairs=12_000)
+    for sc in (Scoring(want_coords=True), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)):
+        assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
+
+
+@pytest.mark.parametrize("match,mismatch,go,ge,affine", [
+    (1, 0, 0, 1, False), (1, -1, 0, 1, False), (5, -4, 0, 3, False), (3, -2, 0, 0, False),
+    (1, -3, 5, 2, True), (2, -1, 3, 1, True), (4, -60, 10, 1, True), (2, 0, 1, 1, True),
+])
+def test_scoring_schemes(gpu_ctx, oracle, match, mismatch, go, ge, affine):
+    b = make_pairs(3000, (1, 200), 1.7, seed=match * 100 + ge, read_stride=208, win_stride=352)
+    sc = Scoring(match=match, mismatch=mismatch, gap_open=go, gap_extend=ge, affine=affine, want_coords=True)
+    assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
+
+
+def test_edge_lengths(gpu_ctx, oracle):
+    """Empty, 1-base, 16k+/-1 boundaries, max read 256, long windows, byte zoo."""
+    rng = np.random.default_rng(17)
+    lens_r = [0, 1, 2, 15, 16, 17, 31, 32, 33, 150, 255, 256, 256, 7, 0, 100]
+    lens_w = [5, 0, 1, 16, 15, 17, 300, 4096, 1, 512, 256, 4096, 1000, 3000, 0, 2]
+    reads, wins = [], []
+    for m, n in zip(lens_r, lens_w):
+        alpha = np.frombuffer(bytes(range(256)), np.uint8) if m % 2 else np.frombuffer(b"ACGTN", np.uint8)
+        reads.append(bytes(rng.choice(alpha, m)))
+        wins.append(bytes(rng.choice(alpha, n)))
+    # plant exact copies so long alignments exist
+    wins[11] = wins[11][:100] + reads[11] + wins[11][356:]
+    wins[12] = reads[12] + wins[12][256:]
+    R, rl, W, wl = mpa.pack_batch(reads * 3, wins * 3)
+    b = B(R, rl, W, wl)
+    for sc in (Scoring(want_coords=True), Scoring(gap_open=2, gap_extend=1, affine=True, want_coords=True)):
+        assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
+
+
+def test_identical_and_all_mismatch(gpu_ctx, oracle):
+    rng = np.random.default_rng(23)
+    seqs = [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 150)) for _ in range(64)]
+    reads = seqs + [b"A" * 150] * 8 + [b"N" * 150] * 8
+    wins = seqs + [b"C" * 300] * 8 + [b"N" * 300] * 8
+    R, rl, W, wl = mpa.pack_batch(reads, wins)
+    b = B(R, rl, W, wl)
+    sc = Scoring(want_coords=True)
+    got = gpu_run(gpu_ctx, b, sc)
+    assert_same(got, oracle_run(oracle, b, sc), True)
+    assert all(got[0][:64] == 300) and all(got[0][64:72] == 0) and all(got[1][64:72] == -1)
+    assert all(got[0][72:] == 300)
+
+
+def test_async_and_chunking_agree(gpu_ctx, oracle):
+    b = config_batch(2, n_pairs=5000, seed_offset=40)
+    sc = Scoring(want_coords=True)
+    want = oracle_run(oracle, b, sc)
+    for chunk in (0, 1, 7, 999, 5000):
+        if chunk == 1:
+            sub = B(b.reads[:50], b.read_len[:50], b.wins[:50], b.win_len[:50])
+            assert_same(gpu_run(gpu_ctx, sub, sc, chunk), tuple(w[:50] for w in want), True)
+        else:
+            assert_same(gpu_run(gpu_ctx, b, sc, chunk), want, True)
+
+
+def test_empty_batch(gpu_ctx):
+    R = np.zeros((0, 16), np.uint8)
+    s, i, j = gpu_ctx.align_batch(R, np.zeros(0, np.uint16), R, np.zeros(0, np.uint16), Scoring(want_coords=True))
+    assert s.shape == (0,)
+
+
+@pytest.mark.parametrize("bad", ["long_read", "long_window", "match", "mismatch", "delta"])
+def test_range_errors(gpu_ctx, bad):
+    R, rl, W, wl = mpa.pack_batch([b"A" * 257 if bad == "long_read" else b"ACGT"],
+                                  [b"A" * 4097 if bad == "long_window" else b"ACGT"])
+    sc = {"match": Scoring(match=65), "mismatch": Scoring(mismatch=1),
+          "delta": Scoring(match=10, mismatch=-55)}.get(bad, Scoring())
+    with pytest.raises(mpa.MswError):
+        gpu_ctx.align_batch(R, rl, W, wl, sc)
+
+
+def test_device_resident_api(gpu_ctx, oracle):
+    """msw_align_batch_device over HBM-resident arrays (the bench path)."""
+    import torch
+    b = config_batch(2, n_pairs=4000, seed_offset=77)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(b, k))).to(dev)
+         for k in ("reads", "wins")}
+    rl = torch.from_numpy(b.read_len.view(np.int16)).to(dev)
+    wl = torch.from_numpy(b.win_len.view(np.int16)).to(dev)
+    score = torch.zeros(b.n_pairs, dtype=torch.int32, device=dev)
+    ei = torch.zeros(b.n_pairs, dtype=torch.int16, device=dev)
+    ej = torch.zeros(b.n_pairs, dtype=torch.int16, device=dev)
+    sc = Scoring(want_coords=True)
+    gpu_ctx.align_batch_device(t["reads"].data_ptr(), rl.data_ptr(), t["wins"].data_ptr(), wl.data_ptr(),
+                               b.reads.shape[1], b.wins.shape[1], b.n_pairs, score.data_ptr(),
+                               int(b.read_len.max()), int(b.win_len.max()), sc, ei.data_ptr(),
+                               ej.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = (score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy())
+    assert_same(got, oracle_run(oracle, b, sc), True)
+
+
+def test_compat_kats(gpu_ctx):
+    for k in json.load(open(os.path.join(GOLDEN, "kat.json")))["compat"]:
+        assert gpu_ctx.compat(k["s1"].encode(), k["s2"].encode(), k["wg"], k["max_groups"]) == k["expected"], k
+
+
+def test_compat_random_vs_oracle(gpu_ctx, oracle):
+    rng = np.random.default_rng(31)
+    for L, wg, mg in [(1, 1024, 0), (1000, 64, 3), (5000, 256, 7), (1 << 20, 1024, 0), (3_000_001, 1024, 0),
+                      (100_000, 64, 5)]:
+        a = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), L))
+        b = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), L + 3))
+        assert gpu_ctx.compat(a, b, wg, mg) == oracle.compat_align(a, b, wg, mg)
+
+
+def test_gpu_align_reference_semantics(gpu_ctx):
+    dev = mpa.get_gpu_devices()[0]
+    assert mpa.gpu_align("ACGTACGT", "ACGTACGT", dev) == 2
+    assert mpa.gpu_align("AAAA", "CCCC", dev) == 0
+    assert mpa.gpu_align("", "ACGT", dev) == 0
+    assert mpa.gpu_align_chunk_self("ACGT" * 200, dev) == 0          # < 1000 bases
+    assert mpa.gpu_align_chunk_self("ACGT" * 300, dev) == 2
+
+
+def test_full_size_properties(gpu_ctx, oracle):
+    """1M pairs (config 3 size): size-independent invariants on all pairs and
+    bit-exact parity on a random sample."""
+    b = config_batch(3)
+    sc = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)
+    s, i, j = gpu_run(gpu_ctx, b, sc)
+    assert (s >= 0).all()
+    zero = s == 0
+    assert ((i == -1) == zero).all() and ((j == -1) == zero).all()
+    assert (i[~zero] < b.read_len[~zero]).all() and (j[~zero] < b.win_len[~zero]).all()
+    assert (s <= 2 * b.read_len.astype(np.int32)).all()
+    rng = np.random.default_rng(0)
+    idx = np.sort(rng.choice(b.n_pairs, 3000, replace=False))
+    sub = B(b.reads[idx], b.read_len[idx], b.wins[idx], b.win_len[idx])
+    assert_same((s[idx], i[idx], j[idx]), oracle_run(oracle, sub, sc), True)
+    # linear score-only on the same million: the best-cell kernel gives the same scores
+    s_lin = gpu_run(gpu_ctx, b, Scoring())[0]
+    s_lin_c = gpu_run(gpu_ctx, b, Scoring(want_coords=True))[0]
+    assert np.array_equal(s_lin, s_lin_c)
