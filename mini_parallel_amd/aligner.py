@@ -169,6 +169,29 @@ class Context:
                                            ctypes.byref(out), max_read_len, max_win_len,
                                            ctypes.c_void_p(stream or None)))
 
+    def prepare_device_launch(self, reads_ptr: int, read_len_ptr: int, wins_ptr: int,
+                              win_len_ptr: int, read_stride: int, win_stride: int, n_pairs: int,
+                              score_ptr: int, max_read_len: int, max_win_len: int,
+                              scoring: Scoring = LINEAR, end_i_ptr: int = 0, end_j_ptr: int = 0,
+                              stream: int = 0):
+        """Bind the arguments of align_batch_device once; returns a zero-argument
+        callable that enqueues one pass (keeps per-launch host cost minimal)."""
+        batch = BatchT(reads_ptr, wins_ptr, read_len_ptr, win_len_ptr, read_stride, win_stride,
+                       n_pairs)
+        out = OutT(score_ptr, end_i_ptr, end_j_ptr)
+        sc = scoring.to_c()
+        fn = lib().msw_align_batch_device
+        args = (self.handle, ctypes.byref(sc), ctypes.byref(batch), ctypes.byref(out),
+                max_read_len, max_win_len, ctypes.c_void_p(stream or None))
+        keep = (batch, out, sc)
+
+        def launch() -> None:
+            _ = keep
+            rc = fn(*args)
+            if rc:
+                check(rc)
+        return launch
+
     def synchronize(self) -> None:
         check(lib().msw_synchronize(self.handle))
 

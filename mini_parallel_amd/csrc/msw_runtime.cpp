@@ -150,6 +150,8 @@ struct msw_ctx {
 namespace {
 
 int set_device(msw_ctx* ctx) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == ctx->device) return MSW_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     return MSW_OK;
 }

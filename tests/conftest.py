@@ -22,7 +22,11 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
-    """One context for the whole GPU session (one process on the card)."""
+    """One context for the whole GPU session (one process on the card).
+
+    torch is imported first so that libmsw.so binds to the same HIP runtime
+    as torch (the bench and the device-resident tests share pointers/streams)."""
+    import torch  # noqa: F401
     from mini_parallel_amd import Context, is_gpu_available
     if not is_gpu_available():
         pytest.fail("-m gpu tests need a GPU and the built libmsw.so (no CPU fallback)")
