@@ -17,12 +17,12 @@ constexpr int kGroupLanes = 16;        // one DPP row
 constexpr int kPairsPerWave = 8;       // 4 groups x 2 packed pairs
 constexpr int kMaxReadLen = 256;       // KR <= 16
 constexpr int kMaxWinLen = 4096;
-constexpr int kLead = 16;              // sentinel words in front of each window stream
+constexpr int kLead = 32;              // sentinel words in front of each window stream
 
-// u32 words per lane-group stream: kLead + (max_win + 15) steps, rounded so that
-// the four groups of a wave start 16 banks apart (stride == 16 mod 32).
+// u32 words per lane-group stream: kLead + (max_win + 31) steps + 1 lookahead,
+// rounded so that the four groups of a wave start 16 banks apart (== 16 mod 32).
 inline uint32_t stream_stride(uint32_t max_win_len) {
-    uint32_t words = kLead + max_win_len + kGroupLanes - 1;
+    uint32_t words = kLead + max_win_len + 2 * kGroupLanes;
     words = (words + 31u) & ~31u;
     return words + 16u;
 }
@@ -41,22 +41,34 @@ struct SwParams {
     uint32_t n_slots;
     uint32_t lds_stride;      // u32 words per lane-group window stream
     uint32_t code_shift;
+    uint32_t win_vec;         // 1: win_stride % 16 == 0 and wins 16-byte aligned
+    uint32_t pairs_blocks;    // mixed grid: leading blocks that use the pairs layout
+    uint32_t slot_base;       // first slot index of this (sub)grid when order == nullptr
     uint32_t match2;          // match, duplicated into both u16 halves
     uint32_t delta2;          // match - mismatch
     uint32_t gap2;            // linear: gap penalty; affine: gap_extend
     uint32_t open_ext2;       // affine: gap_open + gap_extend
 };
 
-// Rows per lane for a read-length bound (ceil(m / 16), at least 1).
-inline int rows_per_lane(uint32_t max_read_len) {
-    int kr = (int)((max_read_len + kGroupLanes - 1) / kGroupLanes);
+// Packed rows per lane for a read-length bound: ceil(m / 16) in the pairs
+// layout, ceil(m / 32) in the split layout (each packed row holds two rows).
+inline int rows_per_lane(uint32_t max_read_len, bool split) {
+    const uint32_t per = split ? 2 * kGroupLanes : kGroupLanes;
+    int kr = (int)((max_read_len + per - 1) / per);
     return kr < 1 ? 1 : kr;
+}
+
+// 16-byte vector loads of the window rows are legal.
+inline uint32_t vec_ok(const void* base, uint64_t stride) {
+    return (stride % 16 == 0 && ((uintptr_t)base & 15) == 0) ? 1u : 0u;
 }
 
 // Dynamic LDS bytes for one 64-lane block.
 inline size_t lds_bytes(uint32_t lds_stride) { return 4u * (size_t)lds_stride * sizeof(uint32_t); }
 
-hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_read_len,
+enum class Layout { kPairs, kSplit, kMixed };
+
+hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, Layout layout,
                      hipStream_t stream);
 
 // smith_waterman_align restated: result must be zeroed before the launch.

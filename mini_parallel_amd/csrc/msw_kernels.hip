@@ -54,29 +54,63 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return __builtin_bit_cast(uint32_t,
                               __builtin_elementwise_maximum(x, __builtin_elementwise_maximum(y, z)));
 }
+// Score tracking max (opaque so the compiler keeps one op per two rows
+// instead of re-associating into a tree).
+__device__ __forceinline__ uint32_t track_max3(uint32_t best, uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(best), "v"(a), "v"(b));
+    return d;
+}
+
 // DPP row_shr:1 inside each 16-lane row; lane 0 of the row reads 0 (bound_ctrl),
 // which is exactly the matrix's zero top boundary for E, F, G and H.
 __device__ __forceinline__ uint32_t shr1_zero(uint32_t src) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src, 0x111, 0xF, 0xF, true);
 }
 
+// Packed (H + match): a full-rate v_add_u32 suffices -- each u16 half stays
+// below 0x7C00 + 64, so no carry crosses into the high half.
+__device__ __forceinline__ uint32_t add_nc(uint32_t a, uint32_t b) { return a + b; }
+
+// Split layout: {lo = dpp.hi, hi = own.lo} in one v_alignbit_b32.
+__device__ __forceinline__ uint32_t hi_to_lo_own_lo_to_hi(uint32_t own, uint32_t dpp) {
+    return __builtin_amdgcn_alignbit(own, dpp, 16);
+}
+
+// Lane-group layouts (template flag SPLIT):
+//  pairs (SPLIT = false): a 16-lane group scores two pairs, pair a in the low
+//      and pair b in the high u16 half; lane l owns rows [l*KR, l*KR+KR) of
+//      both and scores column t - l at step t.  8 pairs per wave.
+//  split (SPLIT = true): a 16-lane group scores one pair; lane l owns rows
+//      [2l*KR, 2l*KR+KR) in the low half and the next KR rows in the high
+//      half, which runs one column behind: low half column t - 2l, high half
+//      t - 2l - 1.  4 pairs per wave: half the work per wave, for batches too
+//      small to give every SIMD two 8-pair waves.
 struct PairMeta {
-    uint32_t pa, pb;  // pair indices (meaningful only when va / vb)
+    uint32_t pa, pb;  // pair indices (the same pair twice in the split layout)
     bool va, vb;
     int ma, mb, na, nb;
 };
 
-__device__ __forceinline__ PairMeta load_meta(const SwParams& p, uint32_t slot_a) {
+template <bool SPLIT>
+__device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t block) {
+    // Branch-free: clamped indices keep every load legal (n_slots >= 1), the
+    // lengths of padding slots are masked to 0 afterwards.
     PairMeta q;
-    const uint32_t slot_b = slot_a + 1;
+    const uint32_t slot_a = SPLIT ? block * 4u + g : block * 8u + 2u * g;
+    const uint32_t slot_b = SPLIT ? slot_a : slot_a + 1;
+    const uint32_t last = p.n_slots - 1;
+    const uint32_t sa = min(slot_a, last), sb = min(slot_b, last);
     q.va = slot_a < p.n_slots;
     q.vb = slot_b < p.n_slots;
-    q.pa = q.va ? (p.order ? p.order[slot_a] : slot_a) : 0u;
-    q.pb = q.vb ? (p.order ? p.order[slot_b] : slot_b) : 0u;
-    q.ma = q.va ? (int)p.read_len[q.pa] : 0;
-    q.mb = q.vb ? (int)p.read_len[q.pb] : 0;
-    q.na = q.va ? (int)p.win_len[q.pa] : 0;
-    q.nb = q.vb ? (int)p.win_len[q.pb] : 0;
+    q.pa = p.order ? p.order[sa] : p.slot_base + sa;
+    q.pb = SPLIT ? q.pa : (p.order ? p.order[sb] : p.slot_base + sb);
+    const int ma = p.read_len[q.pa], na = p.win_len[q.pa];
+    const int mb = SPLIT ? ma : (int)p.read_len[q.pb], nb = SPLIT ? na : (int)p.win_len[q.pb];
+    q.ma = q.va ? ma : 0;
+    q.mb = q.vb ? mb : 0;
+    q.na = q.va ? na : 0;
+    q.nb = q.vb ? nb : 0;
     return q;
 }
 
@@ -86,31 +120,113 @@ __device__ __forceinline__ int wave_max_i32(int v) {
     return v;
 }
 
-// Packed window stream of this lane group in LDS:
-// stream[kLead + c] = code(win_a[c]) | code(win_b[c]) << 16 for column c,
-// sentinels in front (the wavefront's fill columns) and past each window.
+__device__ __forceinline__ uint32_t wcode(uint32_t byte, bool valid, uint32_t shift) {
+    return valid ? (byte << shift) : kWinSentinel;
+}
+
+// Packed window stream of this lane group in LDS, kLead sentinel words first:
+//   pairs: stream[kLead + c] = code(win_a[c]) | code(win_b[c])   << 16
+//   split: stream[kLead + c] = code(win[c])   | code(win[c - 1]) << 16
+// Sentinels past each window.  Vector path: 16-byte loads, a round of up to
+// four chunks of 16 columns per lane in flight together.  Scalar path
+// (unaligned batches): byte loads with clamped addresses, no branches.
+template <bool SPLIT>
 __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& q, uint32_t* stream,
                                              int steps, int lg) {
     const uint8_t* wa = p.wins + (uint64_t)q.pa * p.win_stride;
     const uint8_t* wb = p.wins + (uint64_t)q.pb * p.win_stride;
+    const uint32_t sh = p.code_shift;
+    const int last = (int)p.win_stride - 1;
     stream[lg] = kWinSentinel2;
-    for (int c = lg; c < steps; c += kGroupLanes) {
-        const uint32_t ca = c < q.na ? ((uint32_t)wa[c] << p.code_shift) : kWinSentinel;
-        const uint32_t cb = c < q.nb ? ((uint32_t)wb[c] << p.code_shift) : kWinSentinel;
-        stream[kLead + c] = ca | (cb << 16);
+    stream[lg + kGroupLanes] = kWinSentinel2;
+    const int nch = (steps + 15) >> 4;  // chunks of 16 columns to stage
+    if (p.win_vec) {
+        const int loadable = (int)(p.win_stride >> 4);
+        for (int k0 = 0; k0 < nch; k0 += 4 * kGroupLanes) {
+            uint4 va[4], vb[4];
+            uint32_t prev[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u * kGroupLanes + lg;
+                const bool ld = k < nch && k < loadable;
+                va[u] = ld ? *reinterpret_cast<const uint4*>(wa + 16 * k) : make_uint4(0, 0, 0, 0);
+                if constexpr (SPLIT) {
+                    prev[u] = wa[min(max(16 * k - 1, 0), last)];
+                } else {
+                    vb[u] = ld ? *reinterpret_cast<const uint4*>(wb + 16 * k) : make_uint4(0, 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u * kGroupLanes + lg;
+                if (k < nch) {
+                    const uint32_t xa[4] = {va[u].x, va[u].y, va[u].z, va[u].w};
+                    uint32_t xb[4] = {0u, 0u, 0u, 0u};
+                    if constexpr (!SPLIT) { xb[0] = vb[u].x; xb[1] = vb[u].y; xb[2] = vb[u].z; xb[3] = vb[u].w; }
+                    uint4* dst = reinterpret_cast<uint4*>(stream + kLead + 16 * k);
+                    uint32_t carry = 0u;
+                    if constexpr (SPLIT) carry = prev[u] & 0xFFu;  // byte of column 16k - 1
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        uint32_t w4[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int c = 16 * k + 4 * d + e;
+                            const uint32_t ba = (xa[d] >> (8 * e)) & 0xFFu;
+                            if constexpr (SPLIT) {
+                                w4[e] = wcode(ba, c < q.na, sh) | (wcode(carry, c >= 1 && c - 1 < q.na, sh) << 16);
+                                carry = ba;
+                            } else {
+                                const uint32_t bb = (xb[d] >> (8 * e)) & 0xFFu;
+                                w4[e] = wcode(ba, c < q.na, sh) | (wcode(bb, c < q.nb, sh) << 16);
+                            }
+                        }
+                        dst[d] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                    }
+                }
+            }
+        }
+    } else {
+        for (int c0 = 0; c0 < steps; c0 += 4 * kGroupLanes) {
+            uint32_t ba[4], bb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u * kGroupLanes + lg;
+                ba[u] = wa[min(c, last)];
+                bb[u] = SPLIT ? wa[min(max(c - 1, 0), last)] : wb[min(c, last)];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u * kGroupLanes + lg;
+                const bool vb = SPLIT ? (c >= 1 && c - 1 < q.na) : (c < q.nb);
+                if (c < steps) stream[kLead + c] = wcode(ba[u], c < q.na, sh) | (wcode(bb[u], vb, sh) << 16);
+            }
+        }
     }
 }
 
-template <int KR>
+// Read codes of this lane's packed rows.  Unconditional loads with clamped
+// addresses (all in flight at once), masked afterwards.
+template <int KR, bool SPLIT>
 __device__ __forceinline__ void load_read_codes(const SwParams& p, const PairMeta& q, int lg,
                                                 uint32_t (&rc)[KR]) {
     const uint8_t* ra = p.reads + (uint64_t)q.pa * p.read_stride;
     const uint8_t* rb = p.reads + (uint64_t)q.pb * p.read_stride;
+    const int last = (int)p.read_stride - 1;
+    uint32_t ba[KR], bb[KR];
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
-        const int i = lg * KR + r;
-        const uint32_t ca = i < q.ma ? ((uint32_t)ra[i] << p.code_shift) : kReadSentinel;
-        const uint32_t cb = i < q.mb ? ((uint32_t)rb[i] << p.code_shift) : kReadSentinel;
+        const int ia = SPLIT ? lg * 2 * KR + r : lg * KR + r;
+        const int ib = SPLIT ? ia + KR : ia;
+        ba[r] = ra[min(ia, last)];
+        bb[r] = rb[min(ib, last)];
+    }
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+        const int ia = SPLIT ? lg * 2 * KR + r : lg * KR + r;
+        const int ib = SPLIT ? ia + KR : ia;
+        const uint32_t ca = ia < q.ma ? (ba[r] << p.code_shift) : kReadSentinel;
+        const uint32_t cb = ib < q.mb ? (bb[r] << p.code_shift) : kReadSentinel;
         rc[r] = ca | (cb << 16);
     }
 }
@@ -148,176 +264,180 @@ __device__ __forceinline__ void store_hit(const SwParams& p, bool valid, uint32_
     }
 }
 
-// Per-row keys (h << 16 | 0xFFFF - j, one per packed half) -> group best hits.
-template <int KR>
+// Per-row keys (h << 16 | 0xFFFF - j, one per u16 half) -> best hits.
+template <int KR, bool SPLIT>
 __device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta& q, int lg,
                                               const uint32_t (&key_a)[KR], const uint32_t (&key_b)[KR]) {
     uint64_t ga = 0, gb = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
-        const uint64_t ni = 0xFFFFu - (uint32_t)(lg * KR + r);
-        const uint64_t ka = ((uint64_t)(key_a[r] >> 16) << 32) | (ni << 16) | (key_a[r] & 0xFFFFu);
-        const uint64_t kb = ((uint64_t)(key_b[r] >> 16) << 32) | (ni << 16) | (key_b[r] & 0xFFFFu);
+        const uint32_t ia = SPLIT ? (uint32_t)(lg * 2 * KR + r) : (uint32_t)(lg * KR + r);
+        const uint32_t ib = SPLIT ? ia + KR : ia;
+        const uint64_t ka = ((uint64_t)(key_a[r] >> 16) << 32) | ((uint64_t)(0xFFFFu - ia) << 16) |
+                            (key_a[r] & 0xFFFFu);
+        const uint64_t kb = ((uint64_t)(key_b[r] >> 16) << 32) | ((uint64_t)(0xFFFFu - ib) << 16) |
+                            (key_b[r] & 0xFFFFu);
         ga = ka > ga ? ka : ga;
         gb = kb > gb ? kb : gb;
     }
-    ga = group_max_u64(ga);
-    gb = group_max_u64(gb);
-    if (lg == 0) {
-        store_hit(p, q.va, q.pa, ga);
-        store_hit(p, q.vb, q.pb, gb);
+    if constexpr (SPLIT) {
+        ga = gb > ga ? gb : ga;
+        ga = group_max_u64(ga);
+        if (lg == 0) store_hit(p, q.va, q.pa, ga);
+    } else {
+        ga = group_max_u64(ga);
+        gb = group_max_u64(gb);
+        if (lg == 0) {
+            store_hit(p, q.va, q.pa, ga);
+            store_hit(p, q.vb, q.pb, gb);
+        }
     }
 }
 
-// ---------------------------------------------------------------------------
-// Linear gap.  Per packed cell pair (two pairs, same (i, j)):
-//   a  = min(rc ^ w, delta)        substitution penalty, 0 or match-mismatch
-//   t1 = sat(DG - a)               DG = H_diag + match, so t1 = max(H_diag + s, 0)
-//   h  = max3(t1, E_left, E_up)    E = sat(H - gap)
-//   E  = sat(h - gap); DG(next row, next column) = h + match
-// All t1 of a step are formed first (they only read last step's values), so
-// the H+match of row r can land in the register row r+1 just consumed.
-// ---------------------------------------------------------------------------
-template <int KR, bool COORDS>
-__global__ __launch_bounds__(64) void sw_linear_kernel(SwParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int lane = threadIdx.x;
-    const int g = lane >> 4, lg = lane & 15;
-    const PairMeta q = load_meta(p, blockIdx.x * (uint32_t)kPairsPerWave + 2u * g);
-    const int steps = __builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + kGroupLanes - 1;
-    uint32_t* stream = lds + g * p.lds_stride;
-    stage_window(p, q, stream, steps, lg);
-    uint32_t rc[KR];
-    load_read_codes<KR>(p, q, lg, rc);
-    __syncthreads();
-
-    const uint32_t match2 = p.match2, delta2 = p.delta2, gap2 = p.gap2;
-    uint32_t E[KR], DG[KR];
-    uint32_t key_a[KR], key_b[KR];
-#pragma unroll
-    for (int r = 0; r < KR; ++r) { E[r] = 0u; DG[r] = match2; key_a[r] = 0u; key_b[r] = 0u; }
-    uint32_t e_bot = 0u, h_bot = 0u, d_up_prev = match2;
-    uint32_t best = 0u;
-    // lane lg reads column t - lg: stream index kLead + t - lg (kLead sentinels in front)
-    const uint32_t* wp = stream + (kLead - lg);
-
-    uint32_t w_next = wp[0];  // one step of LDS lookahead
-    for (int t = 0; t < steps; ++t) {
-        const uint32_t w = w_next;
-        w_next = wp[t + 1];
-        const uint32_t e_up = shr1_zero(e_bot);
-        const uint32_t d_up = shr1_zero(h_bot) + match2;   // v_add_u32_dpp; lane 0 -> 0 + match
-        DG[0] = d_up_prev;
-        uint32_t t1[KR];
-#pragma unroll
-        for (int r = 0; r < KR; ++r) t1[r] = pk_satsub(DG[r], pk_min(rc[r] ^ w, delta2));
-        const uint32_t nj = COORDS ? ((uint32_t)(0xFFFF + lg - t) & 0xFFFFu) : 0u;
-        uint32_t up = e_up, hprev = 0u;
-#pragma unroll
-        for (int r = 0; r < KR; ++r) {
-            const uint32_t h = pk_max3(t1[r], E[r], up);
-            up = E[r] = pk_satsub(h, gap2);
-            if (r + 1 < KR) DG[r + 1] = pk_add(h, match2);
-            else h_bot = h;
-            if constexpr (COORDS) {
-                key_a[r] = max(key_a[r], (h << 16) | nj);
-                key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj);
-            } else {
-                if (r & 1) best = pk_max3(best, hprev, h);
-                else if (r + 1 == KR) best = pk_max(best, h);
-                hprev = h;
-            }
-        }
-        e_bot = E[KR - 1];
-        d_up_prev = d_up;
-    }
-
-    if constexpr (COORDS) {
-        finish_coords<KR>(p, q, lg, key_a, key_b);
-    } else {
-        best = group_pk_max(best);
-        if (lg == 0) {
+template <bool SPLIT>
+__device__ __forceinline__ void finish_score(const SwParams& p, const PairMeta& q, int lg, uint32_t best) {
+    best = group_pk_max(best);
+    if (lg == 0) {
+        if constexpr (SPLIT) {
+            store_score(p, q.va, q.pa, max(best & 0xFFFFu, best >> 16));
+        } else {
             store_score(p, q.va, q.pa, best & 0xFFFFu);
             store_score(p, q.vb, q.pb, best >> 16);
         }
     }
 }
 
+// Bottom-row hand-off from lane l-1 (DPP row_shr:1, lane 0 reads the zero top
+// boundary).  Split layout: the low half takes lane l-1's high-half row, the
+// high half takes this lane's own low-half row of the previous step.
+template <bool SPLIT>
+__device__ __forceinline__ uint32_t from_above(uint32_t own_bottom) {
+    const uint32_t d = shr1_zero(own_bottom);
+    if constexpr (SPLIT) return hi_to_lo_own_lo_to_hi(own_bottom, d);
+    else return d;
+}
+
 // ---------------------------------------------------------------------------
-// Affine gap (Gotoh), values floored at 0 (identical H: DESIGN.md proof).
-//   E  = max(sat(E_left - ge), G_left)      G = sat(H - go - ge)
-//   F  = max(sat(F_up - ge),   G_up)
-//   h  = max3(sat(DG - a), E, F)
-//   G  = sat(h - go - ge); DG(next row, next column) = h + match
+// The DP.  Per packed cell pair (same (i, j) in both halves):
+//   linear:  a  = min(rc ^ w, delta)            substitution penalty 0 / delta
+//            t1 = sat(DG - a)                   DG = H_diag + match -> max(H_diag + s, 0)
+//            h  = max3(t1, E_left, E_up)        E = sat(H - gap)
+//   affine:  E  = max(sat(E_left - ge), G_left) G = sat(H - go - ge)
+//            F  = max(sat(F_up - ge),   G_up)
+//            h  = max3(t1, E, F)
+//   DG(next row, next column) = h + match.
+// All t1 of a step are formed first (they only read last step's values), so
+// h + match of row r can land in the register row r+1 just consumed.
 // ---------------------------------------------------------------------------
-template <int KR, bool COORDS>
-__global__ __launch_bounds__(64) void sw_affine_kernel(SwParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
+__device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint32_t* lds) {
     const int lane = threadIdx.x;
     const int g = lane >> 4, lg = lane & 15;
-    const PairMeta q = load_meta(p, blockIdx.x * (uint32_t)kPairsPerWave + 2u * g);
-    const int steps = __builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + kGroupLanes - 1;
+    const PairMeta q = load_meta<SPLIT>(p, g, block);
+    const int skew = SPLIT ? 2 * (kGroupLanes - 1) + 1 : kGroupLanes - 1;
+    const int steps = __builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + skew;
     uint32_t* stream = lds + g * p.lds_stride;
-    stage_window(p, q, stream, steps, lg);
+    stage_window<SPLIT>(p, q, stream, steps, lg);
     uint32_t rc[KR];
-    load_read_codes<KR>(p, q, lg, rc);
+    load_read_codes<KR, SPLIT>(p, q, lg, rc);
     __syncthreads();
 
     const uint32_t match2 = p.match2, delta2 = p.delta2, ext2 = p.gap2, oe2 = p.open_ext2;
-    uint32_t E[KR], G[KR], DG[KR];
-    uint32_t key_a[KR], key_b[KR];
+    uint32_t E[KR], G[AFFINE ? KR : 1], DG[KR];
+    uint32_t key_a[COORDS ? KR : 1], key_b[COORDS ? KR : 1];
 #pragma unroll
-    for (int r = 0; r < KR; ++r) { E[r] = 0u; G[r] = 0u; DG[r] = match2; key_a[r] = 0u; key_b[r] = 0u; }
-    uint32_t f_bot = 0u, g_bot = 0u, h_bot = 0u, d_up_prev = match2;
+    for (int r = 0; r < KR; ++r) {
+        E[r] = 0u;
+        DG[r] = match2;
+        if constexpr (AFFINE) G[r] = 0u;
+        if constexpr (COORDS) { key_a[r] = 0u; key_b[r] = 0u; }
+    }
+    uint32_t f_bot = 0u, h_bot = 0u, d_up_prev = match2;
     uint32_t best = 0u;
-    const uint32_t* wp = stream + (kLead - lg);
+    // lane reads column t - lg (pairs) / t - 2lg (split) at stream index kLead + that
+    const uint32_t* wp = stream + (kLead - (SPLIT ? 2 * lg : lg));
+    const uint32_t nj_lane = (uint32_t)(0xFFFF + (SPLIT ? 2 * lg : lg));
 
     uint32_t w_next = wp[0];  // one step of LDS lookahead
     for (int t = 0; t < steps; ++t) {
         const uint32_t w = w_next;
         w_next = wp[t + 1];
-        uint32_t f = shr1_zero(f_bot);
-        uint32_t g_up = shr1_zero(g_bot);
-        const uint32_t d_up = shr1_zero(h_bot) + match2;
+        const uint32_t d_up = add_nc(from_above<SPLIT>(h_bot), match2);
+        uint32_t up;    // linear: E of the row above; affine: F of the row above
+        uint32_t g_up;  // affine: G of the row above
+        if constexpr (AFFINE) {
+            up = from_above<SPLIT>(f_bot);
+            g_up = from_above<SPLIT>(G[KR - 1]);
+        } else {
+            up = from_above<SPLIT>(E[KR - 1]);
+            g_up = 0u;
+        }
         DG[0] = d_up_prev;
         uint32_t t1[KR];
 #pragma unroll
         for (int r = 0; r < KR; ++r) t1[r] = pk_satsub(DG[r], pk_min(rc[r] ^ w, delta2));
-        const uint32_t nj = COORDS ? ((uint32_t)(0xFFFF + lg - t) & 0xFFFFu) : 0u;
+        const uint32_t nj_a = (nj_lane - (uint32_t)t) & 0xFFFFu;
+        const uint32_t nj_b = SPLIT ? ((nj_lane + 1u - (uint32_t)t) & 0xFFFFu) : nj_a;
         uint32_t hprev = 0u;
 #pragma unroll
         for (int r = 0; r < KR; ++r) {
-            const uint32_t e = pk_max(pk_satsub(E[r], ext2), G[r]);
-            f = pk_max(pk_satsub(f, ext2), g_up);
-            const uint32_t h = pk_max3(t1[r], e, f);
-            E[r] = e;
-            g_up = G[r] = pk_satsub(h, oe2);
-            if (r + 1 < KR) DG[r + 1] = pk_add(h, match2);
+            uint32_t h;
+            if constexpr (AFFINE) {
+                const uint32_t e = pk_max(pk_satsub(E[r], ext2), G[r]);
+                up = pk_max(pk_satsub(up, ext2), g_up);
+                h = pk_max3(t1[r], e, up);
+                E[r] = e;
+                g_up = G[r] = pk_satsub(h, oe2);
+            } else {
+                h = pk_max3(t1[r], E[r], up);
+                up = E[r] = pk_satsub(h, ext2);
+            }
+            if (r + 1 < KR) DG[r + 1] = add_nc(h, match2);
             else h_bot = h;
             if constexpr (COORDS) {
-                key_a[r] = max(key_a[r], (h << 16) | nj);
-                key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj);
+                key_a[r] = max(key_a[r], (h << 16) | nj_a);
+                key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj_b);
             } else {
-                if (r & 1) best = pk_max3(best, hprev, h);
+                if (r & 1) best = track_max3(best, hprev, h);
                 else if (r + 1 == KR) best = pk_max(best, h);
                 hprev = h;
             }
         }
-        f_bot = f;
-        g_bot = G[KR - 1];
+        if constexpr (AFFINE) f_bot = up;
         d_up_prev = d_up;
     }
 
-    if constexpr (COORDS) {
-        finish_coords<KR>(p, q, lg, key_a, key_b);
+    if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, key_a, key_b);
+    else finish_score<SPLIT>(p, q, lg, best);
+}
+
+// One layout for the whole grid.
+template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
+__global__ __launch_bounds__(64) void sw_kernel(SwParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    sw_body<KR, AFFINE, COORDS, SPLIT>(p, blockIdx.x, lds);
+}
+
+// Mixed grid for small batches: blocks [0, p.pairs_blocks) run the pairs
+// layout (8 pairs each, at most one per SIMD), the rest the split layout
+// (4 pairs each) over the remaining slots; the block's layout is uniform.
+// Waves are dispatched in block order, so the split waves fill in beside the
+// pairs waves instead of stacking a second 8-pair wave on some SIMDs.
+template <int KRP, bool AFFINE, bool COORDS>
+__global__ __launch_bounds__(64) void sw_mixed_kernel(SwParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (blockIdx.x < p.pairs_blocks) {
+        sw_body<KRP, AFFINE, COORDS, false>(p, blockIdx.x, lds);
     } else {
-        best = group_pk_max(best);
-        if (lg == 0) {
-            store_score(p, q.va, q.pa, best & 0xFFFFu);
-            store_score(p, q.vb, q.pb, best >> 16);
-        }
+        SwParams q = p;
+        const uint32_t done = p.pairs_blocks * (uint32_t)kPairsPerWave;
+        q.n_slots = p.n_slots - done;
+        q.order = p.order ? p.order + done : nullptr;
+        if (!p.order) q.slot_base = done;
+        sw_body<(KRP + 1) / 2, AFFINE, COORDS, true>(q, blockIdx.x - p.pairs_blocks, lds);
     }
 }
+
 
 // ---------------------------------------------------------------------------
 // smith_waterman_align (smith_waterman.cl:11-71) restated.  Work item (g, t)
@@ -350,43 +470,88 @@ __global__ __launch_bounds__(256) void sw_compat_kernel(const uint8_t* __restric
     if ((threadIdx.x & 63) == 0 && best > 0) atomicMax(result, best);
 }
 
+
 // ---------------------------------------------------------------------------
 // Launchers.
 // ---------------------------------------------------------------------------
-template <int KR>
+template <int KR, bool SPLIT>
 static hipError_t launch_kr(const SwParams& p, bool affine, bool coords, hipStream_t stream) {
-    const dim3 grid((p.n_slots + kPairsPerWave - 1) / kPairsPerWave), block(64);
+    const uint32_t per_wave = SPLIT ? 4u : (uint32_t)kPairsPerWave;
+    const dim3 grid((p.n_slots + per_wave - 1) / per_wave), block(64);
     const size_t shm = lds_bytes(p.lds_stride);
     if (affine) {
-        if (coords) hipLaunchKernelGGL((sw_affine_kernel<KR, true>), grid, block, shm, stream, p);
-        else hipLaunchKernelGGL((sw_affine_kernel<KR, false>), grid, block, shm, stream, p);
+        if (coords) hipLaunchKernelGGL((sw_kernel<KR, true, true, SPLIT>), grid, block, shm, stream, p);
+        else hipLaunchKernelGGL((sw_kernel<KR, true, false, SPLIT>), grid, block, shm, stream, p);
     } else {
-        if (coords) hipLaunchKernelGGL((sw_linear_kernel<KR, true>), grid, block, shm, stream, p);
-        else hipLaunchKernelGGL((sw_linear_kernel<KR, false>), grid, block, shm, stream, p);
+        if (coords) hipLaunchKernelGGL((sw_kernel<KR, false, true, SPLIT>), grid, block, shm, stream, p);
+        else hipLaunchKernelGGL((sw_kernel<KR, false, false, SPLIT>), grid, block, shm, stream, p);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_read_len,
+template <int KRP>
+static hipError_t launch_mixed_kr(const SwParams& p, bool affine, bool coords, uint32_t blocks,
+                                  hipStream_t stream) {
+    const size_t shm = lds_bytes(p.lds_stride);
+    if (affine) {
+        if (coords) hipLaunchKernelGGL((sw_mixed_kernel<KRP, true, true>), dim3(blocks), dim3(64), shm, stream, p);
+        else hipLaunchKernelGGL((sw_mixed_kernel<KRP, true, false>), dim3(blocks), dim3(64), shm, stream, p);
+    } else {
+        if (coords) hipLaunchKernelGGL((sw_mixed_kernel<KRP, false, true>), dim3(blocks), dim3(64), shm, stream, p);
+        else hipLaunchKernelGGL((sw_mixed_kernel<KRP, false, false>), dim3(blocks), dim3(64), shm, stream, p);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, Layout layout,
                      hipStream_t stream) {
     if (p.n_slots == 0) return hipSuccess;
-    switch (rows_per_lane(max_read_len)) {
-        case 1: return launch_kr<1>(p, affine, coords, stream);
-        case 2: return launch_kr<2>(p, affine, coords, stream);
-        case 3: return launch_kr<3>(p, affine, coords, stream);
-        case 4: return launch_kr<4>(p, affine, coords, stream);
-        case 5: return launch_kr<5>(p, affine, coords, stream);
-        case 6: return launch_kr<6>(p, affine, coords, stream);
-        case 7: return launch_kr<7>(p, affine, coords, stream);
-        case 8: return launch_kr<8>(p, affine, coords, stream);
-        case 9: return launch_kr<9>(p, affine, coords, stream);
-        case 10: return launch_kr<10>(p, affine, coords, stream);
-        case 11: return launch_kr<11>(p, affine, coords, stream);
-        case 12: return launch_kr<12>(p, affine, coords, stream);
-        case 13: return launch_kr<13>(p, affine, coords, stream);
-        case 14: return launch_kr<14>(p, affine, coords, stream);
-        case 15: return launch_kr<15>(p, affine, coords, stream);
-        case 16: return launch_kr<16>(p, affine, coords, stream);
+    if (layout == Layout::kMixed) {
+        const uint32_t rest = p.n_slots - min(p.n_slots, p.pairs_blocks * (uint32_t)kPairsPerWave);
+        const uint32_t blocks = p.pairs_blocks + (rest + 3) / 4;
+        switch (rows_per_lane(max_read_len, false)) {
+            case 2: return launch_mixed_kr<2>(p, affine, coords, blocks, stream);
+            case 4: return launch_mixed_kr<4>(p, affine, coords, blocks, stream);
+            case 6: return launch_mixed_kr<6>(p, affine, coords, blocks, stream);
+            case 8: return launch_mixed_kr<8>(p, affine, coords, blocks, stream);
+            case 10: return launch_mixed_kr<10>(p, affine, coords, blocks, stream);
+            case 12: return launch_mixed_kr<12>(p, affine, coords, blocks, stream);
+            case 14: return launch_mixed_kr<14>(p, affine, coords, blocks, stream);
+            case 16: return launch_mixed_kr<16>(p, affine, coords, blocks, stream);
+            default: return hipErrorInvalidValue;  // odd KR: caller picks pairs/split
+        }
+    }
+    const bool split = layout == Layout::kSplit;
+    if (split) {
+        switch (rows_per_lane(max_read_len, true)) {
+            case 1: return launch_kr<1, true>(p, affine, coords, stream);
+            case 2: return launch_kr<2, true>(p, affine, coords, stream);
+            case 3: return launch_kr<3, true>(p, affine, coords, stream);
+            case 4: return launch_kr<4, true>(p, affine, coords, stream);
+            case 5: return launch_kr<5, true>(p, affine, coords, stream);
+            case 6: return launch_kr<6, true>(p, affine, coords, stream);
+            case 7: return launch_kr<7, true>(p, affine, coords, stream);
+            case 8: return launch_kr<8, true>(p, affine, coords, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    switch (rows_per_lane(max_read_len, false)) {
+        case 1: return launch_kr<1, false>(p, affine, coords, stream);
+        case 2: return launch_kr<2, false>(p, affine, coords, stream);
+        case 3: return launch_kr<3, false>(p, affine, coords, stream);
+        case 4: return launch_kr<4, false>(p, affine, coords, stream);
+        case 5: return launch_kr<5, false>(p, affine, coords, stream);
+        case 6: return launch_kr<6, false>(p, affine, coords, stream);
+        case 7: return launch_kr<7, false>(p, affine, coords, stream);
+        case 8: return launch_kr<8, false>(p, affine, coords, stream);
+        case 9: return launch_kr<9, false>(p, affine, coords, stream);
+        case 10: return launch_kr<10, false>(p, affine, coords, stream);
+        case 11: return launch_kr<11, false>(p, affine, coords, stream);
+        case 12: return launch_kr<12, false>(p, affine, coords, stream);
+        case 13: return launch_kr<13, false>(p, affine, coords, stream);
+        case 14: return launch_kr<14, false>(p, affine, coords, stream);
+        case 15: return launch_kr<15, false>(p, affine, coords, stream);
+        case 16: return launch_kr<16, false>(p, affine, coords, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -137,6 +138,7 @@ void free_slot(Slot& s) {
 
 struct msw_ctx {
     int device = 0;
+    int cu_count = 256;
     hipStream_t compute = nullptr, copy = nullptr;
     Slot slots[2];
     hipEvent_t slot_events[4] = {};
@@ -214,6 +216,59 @@ uint64_t default_chunk() {
     return 65536;
 }
 
+// Lane-group layout for one launch (msw_kernels.hip): "pairs" packs two pairs
+// per 16-lane group (8 per wave, least work per cell), "split" gives one pair
+// per group (4 per wave, ~10 % more work per cell, half the work per wave),
+// "mixed" runs up to one pairs-wave per SIMD and the rest as split-waves.
+// The choice minimises a makespan model: waves are dealt round-robin over the
+// 4 x CU SIMDs in block order, a wave costs steps x instructions per step
+// (7.3 per packed row; tools/ubench_valu.hip and profiles/ for the numbers),
+// and a SIMD's time is the sum of its waves' costs.
+// MSW_LAYOUT=pairs|split|mixed overrides (tests use it to cover every path).
+struct LaunchPlan {
+    msw::Layout layout;
+    uint32_t pairs_blocks;
+};
+
+LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const Scheme& sch, int cu_count) {
+    const int krp = msw::rows_per_lane(max_m, false);
+    const bool mixed_ok = (krp % 2) == 0;
+    const uint64_t simds = 4ull * (uint64_t)(cu_count > 0 ? cu_count : 256);
+    double row = 7.3;
+    if (sch.affine) row = 12.5;
+    if (sch.coords) row += 3.0;
+    const double cost_p = (max_n + 15.0) * (krp * row + 5.0);
+    const double cost_s = (max_n + 31.0) * (msw::rows_per_lane(max_m, true) * row + 10.0);
+    auto makespan = [&](uint64_t pairs_waves, uint64_t split_waves) {
+        std::vector<double> load(simds, 0.0);
+        for (uint64_t i = 0; i < pairs_waves; ++i) load[i % simds] += cost_p;
+        for (uint64_t i = pairs_waves; i < pairs_waves + split_waves; ++i) load[i % simds] += cost_s;
+        return *std::max_element(load.begin(), load.end());
+    };
+    const uint64_t all_p = (n_pairs + 7) / 8, all_s = (n_pairs + 3) / 4;
+    LaunchPlan best{msw::Layout::kPairs, 0};
+    double best_t = makespan(all_p, 0);
+    const double t_s = makespan(0, all_s);
+    if (t_s < best_t) { best_t = t_s; best = {msw::Layout::kSplit, 0}; }
+    if (mixed_ok && all_p > simds / 4) {
+        for (uint64_t k = 1; k <= 4; ++k) {
+            const uint64_t pw = std::min<uint64_t>(n_pairs / 8, k * simds / 4);
+            if (pw == 0) continue;
+            const uint64_t rest = n_pairs - pw * 8;
+            const double t = makespan(pw, (rest + 3) / 4);
+            if (t < best_t * 0.995) { best_t = t; best = {msw::Layout::kMixed, (uint32_t)pw}; }
+        }
+    }
+    const char* env = getenv("MSW_LAYOUT");
+    if (env && !strcmp(env, "pairs")) best = {msw::Layout::kPairs, 0};
+    if (env && !strcmp(env, "split")) best = {msw::Layout::kSplit, 0};
+    if (env && !strcmp(env, "mixed")) {
+        if (mixed_ok) best = {msw::Layout::kMixed, (uint32_t)std::min<uint64_t>(n_pairs / 8, simds)};
+        else best = {msw::Layout::kSplit, 0};
+    }
+    return best;
+}
+
 // Buckets of one chunk: pairs grouped by rows-per-lane (read length / 16), and
 // inside a bucket by window length, so every wave runs with tight bounds.
 struct Bucket {
@@ -227,7 +282,7 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
     constexpr int kKeys = 17 * 257;
     std::vector<uint32_t> hist(kKeys + 1, 0);
     auto key_of = [&](uint64_t i) {
-        const int kr = msw::rows_per_lane(rlen[i]);
+        const int kr = msw::rows_per_lane(rlen[i], false);
         const int nb = (wlen[i] + 15) / 16;
         return kr * 257 + nb;
     };
@@ -264,7 +319,10 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.win_stride = win_stride;
         p.n_slots = b.count;
         p.lds_stride = msw::stream_stride(b.max_n);
-        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, ctx->compute));
+        p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+        const LaunchPlan plan = choose_layout(b.count, b.max_m, b.max_n, sch, ctx->cu_count);
+        p.pairs_blocks = plan.pairs_blocks;
+        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan.layout, ctx->compute));
     }
     (void)n;
     return MSW_OK;
@@ -421,6 +479,9 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
     msw_ctx* c = new msw_ctx();
     c->device = ordinal;
     hipError_t e = hipSetDevice(ordinal);
+    hipDeviceProp_t prop;
+    if (e == hipSuccess && hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cu_count = prop.multiProcessorCount;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -502,8 +563,11 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     p.win_stride = b->win_stride;
     p.n_slots = (uint32_t)b->n_pairs;
     p.lds_stride = msw::stream_stride(max_win_len);
+    p.win_vec = msw::vec_ok(p.wins, p.win_stride);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
-    HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, st));
+    const LaunchPlan plan = choose_layout(b->n_pairs, max_read_len, max_win_len, sch, ctx->cu_count);
+    p.pairs_blocks = plan.pairs_blocks;
+    HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st));
     return MSW_OK;
 }
 

@@ -37,6 +37,14 @@ def assert_same(got, want, coords: bool):
                                f"{list(zip(i[bad[:5]], j[bad[:5]]))} oracle {list(zip(wi[bad[:5]], wj[bad[:5]]))}")
 
 
+@pytest.fixture(params=["pairs", "split", "mixed"])
+def layout(request, monkeypatch):
+    """Both lane-group layouts of the kernel (the runtime normally picks one
+    per launch from a makespan model)."""
+    monkeypatch.setenv("MSW_LAYOUT", request.param)
+    return request.param
+
+
 class B:  # minimal batch holder
     def __init__(self, reads, read_len, wins, win_len):
         self.reads, self.read_len, self.wins, self.win_len = reads, read_len, wins, win_len
@@ -51,7 +59,7 @@ def test_device_visible(gpu_ctx):
     ("linear_2_-1_2", Scoring(want_coords=True)),
     ("affine_2_-1_o3_e1", Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)),
 ])
-def test_kat(gpu_ctx, section, sc):
+def test_kat(gpu_ctx, layout, section, sc):
     kats = json.load(open(os.path.join(GOLDEN, "kat.json")))[section]
     R, rl, W, wl = mpa.pack_batch([k["read"].encode() for k in kats], [k["window"].encode() for k in kats])
     s, i, j = gpu_ctx.align_batch(R, rl, W, wl, sc)
@@ -61,7 +69,7 @@ def test_kat(gpu_ctx, section, sc):
 
 @pytest.mark.parametrize("name", ["linear_150x300.npz", "affine_150x300.npz", "mixed_linear.npz"])
 @pytest.mark.parametrize("coords", [False, True])
-def test_golden(gpu_ctx, name, coords):
+def test_golden(gpu_ctx, layout, name, coords):
     z = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
     meta = json.loads(str(z["meta"]))
     sc = Scoring(match=meta["match"], mismatch=meta["mismatch"], gap_open=meta.get("gap_open", 0),
@@ -70,21 +78,21 @@ def test_golden(gpu_ctx, name, coords):
     assert_same(got, (z["score"], z["end_i"], z["end_j"]), coords)
 
 
-def test_config2_linear_score_only(gpu_ctx, oracle):
+def test_config2_linear_score_only(gpu_ctx, layout, oracle):
     """BASELINE config 2 at full size: 10k x (150 bp, 300 bp), linear, score-only."""
     b = config_batch(2)
     sc = Scoring()
     assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), False)
 
 
-def test_config3_affine_coords_sample(gpu_ctx, oracle):
+def test_config3_affine_coords_sample(gpu_ctx, layout, oracle):
     """Config 3 shape (affine + best cell), chunked through the pinned pipeline."""
     b = config_batch(3, n_pairs=40_000)
     sc = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)
     assert_same(gpu_run(gpu_ctx, b, sc, chunk=9_000), oracle_run(oracle, b, sc), True)
 
 
-def test_config5_mixed_lengths(gpu_ctx, oracle):
+def test_config5_mixed_lengths(gpu_ctx, layout, oracle):
     """Config 5 shape: 75-250 bp reads, window 2m, length-bucketed dispatch."""
     b = config_batch(5, n_pairs=12_000)
     for sc in (Scoring(want_coords=True), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)):
@@ -95,13 +103,13 @@ def test_config5_mixed_lengths(gpu_ctx, oracle):
     (1, 0, 0, 1, False), (1, -1, 0, 1, False), (5, -4, 0, 3, False), (3, -2, 0, 0, False),
     (1, -3, 5, 2, True), (2, -1, 3, 1, True), (4, -60, 10, 1, True), (2, 0, 1, 1, True),
 ])
-def test_scoring_schemes(gpu_ctx, oracle, match, mismatch, go, ge, affine):
+def test_scoring_schemes(gpu_ctx, layout, oracle, match, mismatch, go, ge, affine):
     b = make_pairs(3000, (1, 200), 1.7, seed=match * 100 + ge, read_stride=208, win_stride=352)
     sc = Scoring(match=match, mismatch=mismatch, gap_open=go, gap_extend=ge, affine=affine, want_coords=True)
     assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
 
 
-def test_edge_lengths(gpu_ctx, oracle):
+def test_edge_lengths(gpu_ctx, layout, oracle):
     """Empty, 1-base, 16k+/-1 boundaries, max read 256, long windows, byte zoo."""
     rng = np.random.default_rng(17)
     lens_r = [0, 1, 2, 15, 16, 17, 31, 32, 33, 150, 255, 256, 256, 7, 0, 100]
@@ -120,7 +128,7 @@ def test_edge_lengths(gpu_ctx, oracle):
         assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
 
 
-def test_identical_and_all_mismatch(gpu_ctx, oracle):
+def test_identical_and_all_mismatch(gpu_ctx, layout, oracle):
     rng = np.random.default_rng(23)
     seqs = [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 150)) for _ in range(64)]
     reads = seqs + [b"A" * 150] * 8 + [b"N" * 150] * 8
@@ -162,7 +170,7 @@ def test_range_errors(gpu_ctx, bad):
         gpu_ctx.align_batch(R, rl, W, wl, sc)
 
 
-def test_device_resident_api(gpu_ctx, oracle):
+def test_device_resident_api(gpu_ctx, layout, oracle):
     """msw_align_batch_device over HBM-resident arrays (the bench path)."""
     import torch
     b = config_batch(2, n_pairs=4000, seed_offset=77)
