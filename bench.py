@@ -32,8 +32,13 @@ sys.path.insert(0, ROOT)
 
 # Per-gfx950 constants (/opt/skills/guides/MI355X_MICROARCH.md, chip table).
 HBM_PEAK_GBPS = 8000.0
-VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9          # 7.86e13 32-bit lane-ops/s
-OPS_PER_CELL_PAIR = {"linear": 6.5, "linear_coords": 9.5, "affine": 10.5, "affine_coords": 13.5}
+SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+# VALU issue cycles per packed row-step (one wave instruction stream covering
+# 64 lanes x 2 cells = 128 cells), from the instruction mix of each kernel
+# variant and the per-op issue costs measured by tools/ubench_valu.hip
+# (half-rate packed/max ops 4.1 cycles, full-rate xor/add 2.2).
+CYCLES_PER_ROW_STEP = {"linear": 22.85, "linear_coords": 37.2, "affine": 43.35,
+                       "affine_coords": 53.6}
 
 
 def parse():
@@ -133,17 +138,14 @@ def main():
     wall_ms = (time.perf_counter() - t0) * 1e3
     kern_ms = ev0.elapsed_time(ev1)
 
-    t = torch.tensor([wall_ms, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_ms, kern_ms = float(t[0]), float(t[1])
+    from mini_parallel_amd import dist as mdist
+    wall_ms, kern_ms = mdist.max_over_ranks([wall_ms, kern_ms], device=dev)
 
-    # Final score gather to rank 0 over RCCL (outside the timed region).
-    gathered = None
-    if world > 1:
-        parts = [torch.zeros_like(score) for _ in range(world)]
-        dist.all_gather(parts, score)
-        gathered = sum(int(p.numel()) for p in parts)
+    # Final score/coordinate gather over RCCL (outside the timed region): the
+    # only collective of the path.
+    g_score, g_i, g_j = mdist.gather_results(score, ei, ej)
+    gathered = {"pairs": int(g_score.numel()),
+                "score_sum": int(g_score.to(torch.int64).sum().item())}
 
     if rank == 0:
         gpu_scores = score.cpu().numpy()
@@ -155,7 +157,7 @@ def main():
                         + batch.n_pairs * (8 if scoring.want_coords else 4))
         achieved = alg_bytes / avg_launch_s / 1e9
         kernel_gcups = cells / avg_launch_s / 1e9
-        valu_ceiling = VALU_LANE_OPS * 2 / OPS_PER_CELL_PAIR[kind] / 1e9
+        valu_ceiling = 128.0 / CYCLES_PER_ROW_STEP[kind] * SIMDS * CLOCK_HZ / 1e9
         traffic = load_pmc_traffic(f"sw_{'affine' if scoring.affine else 'linear'}_kernel")
 
         cpu = None
@@ -215,7 +217,9 @@ def main():
             "valu": {"binding": True, "kernel_gcups": round(kernel_gcups, 1),
                      "ceiling_gcups": round(valu_ceiling, 1),
                      "frac": round(kernel_gcups / valu_ceiling, 4),
-                     "ops_per_packed_cell_pair": OPS_PER_CELL_PAIR[kind]},
+                     "cycles_per_packed_row_step": CYCLES_PER_ROW_STEP[kind],
+                     "basis": "VALU issue bound of the kernel's instruction mix at 2.4 GHz "
+                              "(DESIGN.md 4.3)"},
             "cpu_baseline": cpu,
             "parity": parity,
             "gathered_scores": gathered,

@@ -1,0 +1,57 @@
+"""Multi-GPU helpers: one process per GPU, batch shards with no data-path
+collective, and the final score/coordinate gather (north_star: RCCL over xGMI
+"only for the final score/coord gather").  The same code runs on the `nccl`
+(RCCL) backend on GPUs and on `gloo` for the CPU tests."""
+from __future__ import annotations
+
+import os
+
+
+def world() -> tuple:
+    """(rank, world_size, local_rank) from the torch.distributed.run env."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def shard_range(n_total: int, rank: int, world_size: int) -> tuple:
+    """Contiguous shard [a, b) of a global batch of n_total pairs."""
+    a = n_total * rank // world_size
+    b = n_total * (rank + 1) // world_size
+    return a, b
+
+
+def max_over_ranks(values, device=None):
+    """Element-wise max of a list of floats over all ranks (timing)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
+def gather_results(*tensors):
+    """Gather per-rank result tensors (equal or unequal lengths) to every rank,
+    concatenated in rank order.  Unequal shards are padded to the longest and
+    trimmed after the all_gather (one collective per tensor)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [t for t in tensors]
+    ws = dist.get_world_size()
+    dev = tensors[0].device
+    n = torch.tensor([tensors[0].numel()], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    mx = max(ns)
+    out = []
+    for t in tensors:
+        # neither RCCL nor gloo moves int16: ship 16-bit results as int32
+        wire = torch.int32 if t.dtype in (torch.int16, torch.uint16) else t.dtype
+        pad = torch.zeros(mx, dtype=wire, device=dev)
+        pad[: t.numel()] = t.reshape(-1).to(wire)
+        parts = [torch.zeros_like(pad) for _ in range(ws)]
+        dist.all_gather(parts, pad)
+        out.append(torch.cat([p[:k] for p, k in zip(parts, ns)]).to(t.dtype))
+    return out
