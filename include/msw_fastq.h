@@ -1,0 +1,49 @@
+/*
+ * msw_fastq.h -- FASTQ(.gz) chunk reader of the MI355X scorer (C ABI).
+ *
+ * Replaces process_fastq_file_in_chunks (smith_waterman/src/aligner.rs:107-178)
+ * and count_bases_in_fastq (:535-544).  Same record semantics:
+ *   - a line is the bytes up to '\n' with a trailing "\r" stripped (Rust
+ *     BufRead::lines, :133);
+ *   - a line that is not valid UTF-8 is a read error: it is skipped and not
+ *     counted (:155-158); more than 10 errors abort the file (:160-162);
+ *   - the sequence line is the 1-based line number with line % 4 == 2 (:138);
+ *     headers and '+' lines are not validated;
+ *   - full chunks of N reads, then one final partial chunk (:143-147, :168-170).
+ * Instead of a Vec<String> per chunk, sequences are written straight into a
+ * caller-provided padded SoA slab (e.g. msw_host_alloc'ed pinned memory), the
+ * layout msw_align_batch takes.  .gz files (multi-member included) are read
+ * with zlib in-process (the reference spawns `zcat`, :111-115).
+ */
+#ifndef MSW_FASTQ_H
+#define MSW_FASTQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct msw_fastq msw_fastq;
+
+int msw_fastq_open(const char* path, msw_fastq** out);
+void msw_fastq_close(msw_fastq* fq);
+
+/* Read up to max_reads sequence lines into seqs[i*stride ..], lens[i].
+ * *n_read = reads delivered (0 at end of file).  A sequence longer than
+ * stride is MSW_E_RANGE.  pos (optional, may be NULL): the integer after
+ * "pos=" in the record's header line, -1 when absent (synthetic datasets tag
+ * each read with its reference window offset). */
+int msw_fastq_next(msw_fastq* fq, uint8_t* seqs, uint16_t* lens, uint32_t stride,
+                   uint64_t max_reads, uint64_t* n_read, int64_t* pos);
+
+/* Counters so far: lines (valid lines, aligner.rs:136), reads, read errors. */
+void msw_fastq_stats(const msw_fastq* fq, uint64_t* lines, uint64_t* reads, uint64_t* errors);
+
+/* count_bases_in_fastq (aligner.rs:535-544): total bases and reads. */
+int msw_fastq_count_bases(const char* path, uint64_t* bases, uint64_t* reads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSW_FASTQ_H */

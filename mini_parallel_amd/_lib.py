@@ -26,6 +26,9 @@ EXPORTED = (
     "msw_align_compat", "msw_host_alloc", "msw_host_free", "msw_dev_alloc", "msw_dev_free",
     "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
 )
+# include/msw_fastq.h
+FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_stats",
+                  "msw_fastq_count_bases")
 
 
 class MswError(RuntimeError):
@@ -90,6 +93,14 @@ def _declare(L):
         "msw_synchronize": (I, [P]),
         "msw_last_error": (ctypes.c_char_p, []),
         "msw_version": (ctypes.c_char_p, []),
+        "msw_fastq_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "msw_fastq_close": (None, [P]),
+        "msw_fastq_next": (I, [P, P, P, ctypes.c_uint32, ctypes.c_uint64,
+                               ctypes.POINTER(ctypes.c_uint64), P]),
+        "msw_fastq_stats": (None, [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                   ctypes.POINTER(ctypes.c_uint64)]),
+        "msw_fastq_count_bases": (I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

@@ -1,0 +1,244 @@
+// msw_fastq.cpp -- FASTQ(.gz) chunk reader (include/msw_fastq.h).
+//
+// Semantics of process_fastq_file_in_chunks (aligner.rs:107-178); see the
+// header.  One reader per lane file; no per-line allocation: records are
+// parsed out of a 4 MiB decompressed block buffer and sequences are copied
+// straight into the caller's SoA slab.
+#include <zlib.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/msw.h"
+#include "../../include/msw_fastq.h"
+
+namespace msw_detail {
+// Shared with msw_runtime.cpp: sets the thread-local msw_last_error message.
+int set_error(int code, const char* fmt, ...);
+}  // namespace msw_detail
+
+using msw_detail::set_error;
+
+struct msw_fastq {
+    gzFile gz = nullptr;      // zlib reads plain files transparently too
+    std::vector<char> buf;    // decompressed bytes
+    size_t head = 0, tail = 0;
+    bool eof = false;
+    std::string carry;        // partial line across buffer refills
+    std::string last;         // final line of a file without a trailing newline
+    uint64_t lines = 0, reads = 0, errors = 0;
+    int64_t pending_pos = -1; // pos= tag of the current record's header
+    std::string path;
+};
+
+namespace {
+
+constexpr size_t kBlock = 4u << 20;
+
+// Strict UTF-8 validation (what Rust's String conversion in lines() checks).
+bool valid_utf8(const unsigned char* s, size_t n) {
+    size_t i = 0;
+    while (i < n) {
+        unsigned char c = s[i];
+        if (c < 0x80) { ++i; continue; }
+        size_t len;
+        uint32_t cp;
+        if ((c & 0xE0) == 0xC0) { len = 2; cp = c & 0x1F; }
+        else if ((c & 0xF0) == 0xE0) { len = 3; cp = c & 0x0F; }
+        else if ((c & 0xF8) == 0xF0) { len = 4; cp = c & 0x07; }
+        else return false;
+        if (i + len > n) return false;
+        for (size_t k = 1; k < len; ++k) {
+            if ((s[i + k] & 0xC0) != 0x80) return false;
+            cp = (cp << 6) | (s[i + k] & 0x3F);
+        }
+        if ((len == 2 && cp < 0x80) || (len == 3 && cp < 0x800) || (len == 4 && cp < 0x10000) ||
+            cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF))
+            return false;
+        i += len;
+    }
+    return true;
+}
+
+int64_t parse_pos(const char* s, size_t n) {
+    for (size_t i = 0; i + 4 <= n; ++i) {
+        if (memcmp(s + i, "pos=", 4) == 0) {
+            size_t j = i + 4;
+            bool neg = j < n && s[j] == '-';
+            if (neg) ++j;
+            int64_t v = 0;
+            bool any = false;
+            while (j < n && s[j] >= '0' && s[j] <= '9') { v = v * 10 + (s[j] - '0'); ++j; any = true; }
+            if (any) return neg ? -v : v;
+        }
+    }
+    return -1;
+}
+
+// Next raw line (without '\n'); false at end of data or on an I/O error
+// (*io_err set).  The pointer stays valid until the next call.
+bool next_line(msw_fastq* fq, const char** line, size_t* len, int* io_err) {
+    for (;;) {
+        if (fq->head < fq->tail) {
+            const char* start = fq->buf.data() + fq->head;
+            const char* nl = (const char*)memchr(start, '\n', fq->tail - fq->head);
+            if (nl) {
+                const size_t n = (size_t)(nl - start);
+                fq->head += n + 1;
+                if (!fq->carry.empty()) {
+                    fq->last.assign(fq->carry);
+                    fq->last.append(start, n);
+                    fq->carry.clear();
+                    *line = fq->last.data();
+                    *len = fq->last.size();
+                } else {
+                    *line = start;
+                    *len = n;
+                }
+                return true;
+            }
+            fq->carry.append(start, fq->tail - fq->head);
+            fq->head = fq->tail;
+        }
+        if (fq->eof) {
+            if (fq->carry.empty()) return false;
+            fq->last.swap(fq->carry);  // last line without a newline
+            fq->carry.clear();
+            *line = fq->last.data();
+            *len = fq->last.size();
+            return true;
+        }
+        const int got = gzread(fq->gz, fq->buf.data(), (unsigned)kBlock);
+        if (got < 0) {
+            *io_err = 1;
+            return false;
+        }
+        if (got == 0) fq->eof = true;
+        fq->head = 0;
+        fq->tail = (size_t)got;
+    }
+}
+
+// Next sequence line (1-based line % 4 == 2) with aligner.rs:133-165 rules.
+// Returns 1 with the bytes, 0 at end of file, or a negative MSW error.
+int next_sequence(msw_fastq* fq, const char** seq, size_t* len, int64_t* pos, bool want_pos) {
+    for (;;) {
+        const char* line;
+        size_t n;
+        int io_err = 0;
+        if (!next_line(fq, &line, &n, &io_err)) {
+            if (!io_err) return 0;
+            int zerr = 0;
+            const char* msg = gzerror(fq->gz, &zerr);
+            if (++fq->errors > 10)
+                return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
+                                 (unsigned long long)fq->lines);
+            return set_error(MSW_E_INVALID, "Error reading %s: %s", fq->path.c_str(), msg ? msg : "");
+        }
+        if (n && line[n - 1] == '\r') --n;  // CRLF, as BufRead::lines
+        if (!valid_utf8((const unsigned char*)line, n)) {
+            if (++fq->errors > 10)
+                return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
+                                 (unsigned long long)fq->lines);
+            continue;  // aligner.rs:155-163: skipped and not counted
+        }
+        ++fq->lines;
+        const uint64_t phase = fq->lines % 4;
+        if (phase == 1) {
+            fq->pending_pos = want_pos ? parse_pos(line, n) : -1;
+        } else if (phase == 2) {
+            *seq = line;
+            *len = n;
+            *pos = fq->pending_pos;
+            fq->pending_pos = -1;
+            ++fq->reads;
+            return 1;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int msw_fastq_open(const char* path, msw_fastq** out) {
+    if (!path || !out) return set_error(MSW_E_INVALID, "path/out is NULL");
+    *out = nullptr;
+    gzFile gz = gzopen(path, "rb");
+    if (!gz) return set_error(MSW_E_INVALID, "Failed to open file %s", path);
+    gzbuffer(gz, 1u << 20);
+    msw_fastq* fq = new msw_fastq();
+    fq->gz = gz;
+    fq->buf.resize(kBlock);
+    fq->path = path;
+    *out = fq;
+    return MSW_OK;
+}
+
+void msw_fastq_close(msw_fastq* fq) {
+    if (!fq) return;
+    if (fq->gz) gzclose(fq->gz);
+    delete fq;
+}
+
+int msw_fastq_next(msw_fastq* fq, uint8_t* seqs, uint16_t* lens, uint32_t stride, uint64_t max_reads,
+                   uint64_t* n_read, int64_t* pos) {
+    if (!fq || !n_read || (max_reads && (!seqs || !lens)))
+        return set_error(MSW_E_INVALID, "NULL argument");
+    *n_read = 0;
+    uint64_t n = 0;
+    while (n < max_reads) {
+        const char* seq;
+        size_t len;
+        int64_t p;
+        const int rc = next_sequence(fq, &seq, &len, &p, pos != nullptr);
+        if (rc < 0) return rc;
+        if (rc == 0) break;
+        if (len > stride || len > 0xFFFF)
+            return set_error(MSW_E_RANGE, "sequence of %zu bases at line %llu exceeds slab stride %u", len,
+                             (unsigned long long)fq->lines, stride);
+        uint8_t* dst = seqs + n * (uint64_t)stride;
+        memcpy(dst, seq, len);
+        if (len < stride) memset(dst + len, 0, stride - len);
+        lens[n] = (uint16_t)len;
+        if (pos) pos[n] = p;
+        ++n;
+    }
+    *n_read = n;
+    return MSW_OK;
+}
+
+void msw_fastq_stats(const msw_fastq* fq, uint64_t* lines, uint64_t* reads, uint64_t* errors) {
+    if (!fq) return;
+    if (lines) *lines = fq->lines;
+    if (reads) *reads = fq->reads;
+    if (errors) *errors = fq->errors;
+}
+
+int msw_fastq_count_bases(const char* path, uint64_t* bases, uint64_t* reads) {
+    if (!bases) return set_error(MSW_E_INVALID, "bases is NULL");
+    msw_fastq* fq = nullptr;
+    int rc = msw_fastq_open(path, &fq);
+    if (rc) return rc;
+    uint64_t total = 0, nr = 0;
+    for (;;) {
+        const char* seq;
+        size_t len;
+        int64_t p;
+        rc = next_sequence(fq, &seq, &len, &p, false);
+        if (rc < 0) { msw_fastq_close(fq); return rc; }
+        if (rc == 0) break;
+        total += len;  // Rust String::len = bytes (aligner.rs:540)
+        ++nr;
+    }
+    msw_fastq_close(fq);
+    *bases = total;
+    if (reads) *reads = nr;
+    return MSW_OK;
+}
+
+}  // extern "C"

@@ -39,6 +39,22 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+namespace msw_detail {
+int set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+}  // namespace msw_detail
+
+namespace {
+
 #define HIP_TRY(expr)                                                                          \
     do {                                                                                       \
         hipError_t e_ = (expr);                                                                \
@@ -127,10 +143,12 @@ struct Slot {
 };
 
 void free_slot(Slot& s) {
-    hipFree(s.d_reads); hipFree(s.d_wins); hipFree(s.d_rlen); hipFree(s.d_wlen);
-    hipFree(s.d_order); hipFree(s.d_score); hipFree(s.d_ei); hipFree(s.d_ej);
-    hipHostFree(s.h_reads); hipHostFree(s.h_wins); hipHostFree(s.h_rlen); hipHostFree(s.h_wlen);
-    hipHostFree(s.h_order); hipHostFree(s.h_score); hipHostFree(s.h_ei); hipHostFree(s.h_ej);
+    for (void* p : {(void*)s.d_reads, (void*)s.d_wins, (void*)s.d_rlen, (void*)s.d_wlen, (void*)s.d_order,
+                    (void*)s.d_score, (void*)s.d_ei, (void*)s.d_ej})
+        if (p) (void)hipFree(p);
+    for (void* p : {(void*)s.h_reads, (void*)s.h_wins, (void*)s.h_rlen, (void*)s.h_wlen, (void*)s.h_order,
+                    (void*)s.h_score, (void*)s.h_ei, (void*)s.h_ej})
+        if (p) (void)hipHostFree(p);
     s = Slot{};
 }
 
@@ -160,7 +178,7 @@ int set_device(msw_ctx* ctx) {
 
 template <typename T>
 int grow_dev(T** p, size_t n) {
-    hipFree(*p);
+    if (*p) (void)hipFree(*p);
     *p = nullptr;
     if (n == 0) return MSW_OK;
     hipError_t e = hipMalloc((void**)p, n * sizeof(T));
@@ -169,7 +187,7 @@ int grow_dev(T** p, size_t n) {
 }
 template <typename T>
 int grow_host(T** p, size_t n) {
-    hipHostFree(*p);
+    if (*p) (void)hipHostFree(*p);
     *p = nullptr;
     if (n == 0) return MSW_OK;
     hipError_t e = hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault);
@@ -329,13 +347,14 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
 }
 
 // Copy finished results of a slot into the caller's arrays.
-void drain_slot(Slot& s) {
-    if (!s.busy) return;
-    hipEventSynchronize(s.done);
+int drain_slot(Slot& s) {
+    if (!s.busy) return MSW_OK;
+    s.busy = false;
+    HIP_TRY(hipEventSynchronize(s.done));
     memcpy(s.out.score + s.first, s.h_score, s.count * sizeof(int32_t));
     if (s.out.end_i) memcpy(s.out.end_i + s.first, s.h_ei, s.count * sizeof(int16_t));
     if (s.out.end_j) memcpy(s.out.end_j + s.first, s.h_ej, s.count * sizeof(int16_t));
-    s.busy = false;
+    return MSW_OK;
 }
 
 int validate_batch(const msw_batch_t* b, const msw_out_t* out, const Scheme& sch) {
@@ -376,7 +395,7 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* b, msw_o
     for (uint64_t first = 0; first < n; first += chunk, ++c) {
         const uint64_t cnt = std::min(chunk, n - first);
         Slot& s = ctx->slots[c & 1];
-        drain_slot(s);  // the slot's previous chunk must be out before reuse
+        if ((rc = drain_slot(s))) return rc;  // the slot's previous chunk must be out before reuse
         if ((rc = ensure_slot(s, cnt, cnt * b->read_stride, cnt * b->win_stride))) return rc;
         // Stage the chunk in pinned memory.  (FASTQ callers fill these slabs
         // directly; see msw_fastq.cpp.)
@@ -419,8 +438,7 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* b, msw_o
         if (!sch.coords) { s.out.end_i = nullptr; s.out.end_j = nullptr; }
     }
     if (sync) {
-        drain_slot(ctx->slots[0]);
-        drain_slot(ctx->slots[1]);
+        if ((rc = drain_slot(ctx->slots[0])) || (rc = drain_slot(ctx->slots[1]))) return rc;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
     }
@@ -460,11 +478,11 @@ int msw_device_info(int ordinal, msw_device_info_t* out) {
     out->max_wg = (uint32_t)prop.maxThreadsPerBlock;
     out->cu_count = (uint32_t)prop.multiProcessorCount;
     int cur = 0;
-    hipGetDevice(&cur);
+    (void)hipGetDevice(&cur);
     if (hipSetDevice(ordinal) == hipSuccess) {
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) == hipSuccess) out->mem_free_bytes = fr;
-        hipSetDevice(cur);
+        (void)hipSetDevice(cur);
     }
     return MSW_OK;
 }
@@ -494,19 +512,19 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
 
 void msw_ctx_destroy(msw_ctx* ctx) {
     if (!ctx) return;
-    hipSetDevice(ctx->device);
-    if (ctx->compute) hipStreamSynchronize(ctx->compute);
-    if (ctx->copy) hipStreamSynchronize(ctx->copy);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->compute) (void)hipStreamSynchronize(ctx->compute);
+    if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
     for (Slot& s : ctx->slots) {
-        if (s.uploaded) hipEventDestroy(s.uploaded);
-        if (s.done) hipEventDestroy(s.done);
+        if (s.uploaded) (void)hipEventDestroy(s.uploaded);
+        if (s.done) (void)hipEventDestroy(s.done);
         free_slot(s);
     }
-    hipFree(ctx->c_s1);
-    hipFree(ctx->c_s2);
-    hipFree(ctx->c_res);
-    if (ctx->compute) hipStreamDestroy(ctx->compute);
-    if (ctx->copy) hipStreamDestroy(ctx->copy);
+    (void)hipFree(ctx->c_s1);
+    (void)hipFree(ctx->c_s2);
+    (void)hipFree(ctx->c_res);
+    if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
+    if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     delete ctx;
 }
 
@@ -530,8 +548,7 @@ int msw_wait(msw_ctx* ctx, uint64_t ticket) {
     int rc = set_device(ctx);
     if (rc) return rc;
     // Tickets complete in order: draining both slots completes every earlier ticket.
-    drain_slot(ctx->slots[0]);
-    drain_slot(ctx->slots[1]);
+    if ((rc = drain_slot(ctx->slots[0])) || (rc = drain_slot(ctx->slots[1]))) return rc;
     ctx->done_ticket = ctx->next_ticket - 1;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
@@ -615,7 +632,7 @@ void* msw_host_alloc(size_t bytes) {
 }
 
 void msw_host_free(void* p) {
-    if (p) hipHostFree(p);
+    if (p) (void)hipHostFree(p);
 }
 
 void* msw_dev_alloc(msw_ctx* ctx, size_t bytes) {
@@ -629,8 +646,8 @@ void* msw_dev_alloc(msw_ctx* ctx, size_t bytes) {
 }
 
 void msw_dev_free(msw_ctx* ctx, void* p) {
-    if (ctx) hipSetDevice(ctx->device);
-    if (p) hipFree(p);
+    if (ctx) (void)hipSetDevice(ctx->device);
+    if (p) (void)hipFree(p);
 }
 
 int msw_memcpy_h2d(msw_ctx* ctx, void* dst, const void* src, size_t bytes) {

@@ -1,0 +1,81 @@
+"""FASTQ(.gz) chunk loader over the C++ reader (include/msw_fastq.h).
+
+Mirrors aligner.rs:107-178 (process_fastq_file_in_chunks) and :535-544
+(count_bases_in_fastq): same record rules, same chunking, same error budget;
+sequences land in padded SoA numpy slabs (pinned when ``pinned=True``), the
+layout Context.align_batch consumes."""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, Optional
+
+import numpy as np
+
+from ._lib import MswError, check, lib
+
+
+class FastqReader:
+    """Streaming reader of one lane file."""
+
+    def __init__(self, path: str):
+        self.path = path
+        h = ctypes.c_void_p()
+        check(lib().msw_fastq_open(path.encode(), ctypes.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            lib().msw_fastq_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def next_chunk(self, max_reads: int, stride: int = 256, with_pos: bool = False):
+        """Up to max_reads sequences -> (seqs u8[n, stride], lens u16[n][, pos i64[n]])."""
+        seqs = np.zeros((max_reads, stride), np.uint8)
+        lens = np.zeros(max_reads, np.uint16)
+        pos = np.zeros(max_reads, np.int64) if with_pos else None
+        n = ctypes.c_uint64(0)
+        check(lib().msw_fastq_next(self._h, seqs.ctypes.data, lens.ctypes.data, stride, max_reads,
+                                   ctypes.byref(n), pos.ctypes.data if pos is not None else None))
+        k = n.value
+        if with_pos:
+            return seqs[:k], lens[:k], pos[:k]
+        return seqs[:k], lens[:k]
+
+    def stats(self) -> dict:
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib().msw_fastq_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return {"lines": a.value, "reads": b.value, "errors": c.value}
+
+
+def process_fastq_file_in_chunks(filepath: str, chunk_size_reads: int,
+                                 processor: Callable[[list], Optional[object]], stride: int = 4096) -> None:
+    """aligner.rs:107-178: call ``processor`` with lists of sequence strings,
+    full chunks of chunk_size_reads then one final partial chunk.  (For the
+    GPU path use FastqReader.next_chunk, which fills SoA slabs directly.)"""
+    if chunk_size_reads <= 0:
+        raise MswError(-1, "chunk_size_reads must be positive")
+    with FastqReader(filepath) as fq:
+        while True:
+            seqs, lens = fq.next_chunk(chunk_size_reads, stride)
+            if len(lens) == 0:
+                break
+            processor([bytes(seqs[i, :lens[i]]).decode() for i in range(len(lens))])
+
+
+def count_bases_in_fastq(filepath: str) -> int:
+    """aligner.rs:535-544."""
+    bases, reads = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().msw_fastq_count_bases(filepath.encode(), ctypes.byref(bases), ctypes.byref(reads)))
+    return int(bases.value)

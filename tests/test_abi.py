@@ -13,15 +13,19 @@ from mini_parallel_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "msw.h")
+FASTQ_HEADER = os.path.join(ROOT, "include", "msw_fastq.h")
 
 
-def declared_symbols():
-    text = open(HEADER).read()
-    return set(re.findall(r"\b(msw_[a-z0-9_]+)\s*\(", text)) - {"msw_ctx"}
+def declared_symbols(header=None):
+    if header is None:
+        return declared_symbols(HEADER) | declared_symbols(FASTQ_HEADER)
+    text = open(header).read()
+    return set(re.findall(r"\b(msw_[a-z0-9_]+)\s*\(", text)) - {"msw_ctx", "msw_fastq"}
 
 
 def test_header_matches_binding():
-    assert declared_symbols() == set(_lib.EXPORTED)
+    assert declared_symbols(HEADER) == set(_lib.EXPORTED)
+    assert declared_symbols(FASTQ_HEADER) == set(_lib.FASTQ_EXPORTED)
 
 
 def test_library_exports_every_symbol():

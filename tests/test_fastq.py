@@ -1,0 +1,134 @@
+"""FASTQ loader vs a plain-Python restatement of aligner.rs:107-178 (CPU)."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from mini_parallel_amd import MswError
+from mini_parallel_amd.fastq import FastqReader, count_bases_in_fastq, process_fastq_file_in_chunks
+
+
+def reference_chunks(data: bytes, n: int):
+    """aligner.rs:128-170 restated: BufRead::lines (strip \\n and \\r\\n), invalid
+    UTF-8 lines are errors that are skipped and not counted, line % 4 == 2 is
+    the sequence, chunks of n then a final partial one; >10 errors -> Err."""
+    lines = data.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    chunks, chunk, count, errors = [], [], 0, 0
+    for raw in lines:
+        if raw.endswith(b"\r"):
+            raw = raw[:-1]
+        try:
+            s = raw.decode("utf-8")
+        except UnicodeDecodeError:
+            errors += 1
+            if errors > 10:
+                raise ValueError("too many errors")
+            continue
+        count += 1
+        if count % 4 == 2:
+            chunk.append(s)
+            if len(chunk) >= n:
+                chunks.append(chunk)
+                chunk = []
+    if chunk:
+        chunks.append(chunk)
+    return chunks
+
+
+def write(path, data: bytes, gz: bool, members: int = 1):
+    if gz:
+        with open(path, "wb") as f:
+            step = max(1, len(data) // members)
+            for k in range(members):
+                part = data[k * step:(k + 1) * step] if k < members - 1 else data[k * step:]
+                f.write(gzip.compress(part))
+    else:
+        open(path, "wb").write(data)
+
+
+def synth_fastq(n, rng, crlf=False, bad_utf8_at=(), final_newline=True):
+    out = []
+    for i in range(n):
+        seq = bytes(rng.choice(np.frombuffer(b"ACGTN", np.uint8), int(rng.integers(0, 300))))
+        rec = [b"@r%d pos=%d" % (i, i * 7), seq, b"+", b"I" * len(seq)]
+        if i in bad_utf8_at:
+            rec[1] = b"\xff\xfe" + seq
+        out.extend(rec)
+    nl = b"\r\n" if crlf else b"\n"
+    data = nl.join(out)
+    return data + nl if final_newline else data
+
+
+@pytest.mark.parametrize("gz,members", [(False, 1), (True, 1), (True, 3)])
+@pytest.mark.parametrize("crlf", [False, True])
+@pytest.mark.parametrize("final_newline", [True, False])
+def test_chunks_match_reference(tmp_path, gz, members, crlf, final_newline):
+    rng = np.random.default_rng(1)
+    data = synth_fastq(257, rng, crlf=crlf, final_newline=final_newline)
+    p = str(tmp_path / ("x.fastq.gz" if gz else "x.fastq"))
+    write(p, data, gz, members)
+    got = []
+    process_fastq_file_in_chunks(p, 50, got.append)
+    assert got == reference_chunks(data, 50)
+    assert count_bases_in_fastq(p) == sum(len(s) for c in got for s in c)
+
+
+def test_invalid_utf8_lines_shift_phase(tmp_path):
+    rng = np.random.default_rng(2)
+    data = synth_fastq(40, rng, bad_utf8_at=(3, 9))
+    p = str(tmp_path / "bad.fastq")
+    write(p, data, False)
+    got = []
+    process_fastq_file_in_chunks(p, 7, got.append)
+    assert got == reference_chunks(data, 7)
+    with FastqReader(p) as fq:
+        while len(fq.next_chunk(100, stride=512)[1]):
+            pass
+        assert fq.stats()["errors"] == 2
+
+
+def test_too_many_errors(tmp_path):
+    rng = np.random.default_rng(3)
+    data = synth_fastq(30, rng, bad_utf8_at=tuple(range(11)))
+    p = str(tmp_path / "worse.fastq")
+    write(p, data, False)
+    with pytest.raises(MswError, match="Too many read errors"):
+        process_fastq_file_in_chunks(p, 5, lambda c: None)
+
+
+def test_pos_tags_and_slab(tmp_path):
+    rng = np.random.default_rng(4)
+    data = synth_fastq(20, rng)
+    p = str(tmp_path / "t.fastq.gz")
+    write(p, data, True)
+    with FastqReader(p) as fq:
+        seqs, lens, pos = fq.next_chunk(100, stride=304, with_pos=True)
+    assert list(pos) == [i * 7 for i in range(20)]
+    ref = [s for c in reference_chunks(data, 100) for s in c]
+    for i, s in enumerate(ref):
+        assert bytes(seqs[i, :lens[i]]).decode() == s
+        assert not seqs[i, lens[i]:].any()
+
+
+def test_stride_too_small(tmp_path):
+    p = str(tmp_path / "long.fastq")
+    write(p, b"@a\n" + b"A" * 100 + b"\n+\n" + b"I" * 100 + b"\n", False)
+    with FastqReader(p) as fq:
+        with pytest.raises(MswError):
+            fq.next_chunk(10, stride=64)
+
+
+def test_missing_file():
+    with pytest.raises(MswError, match="Failed to open"):
+        FastqReader("/nonexistent/x.fastq.gz")
+
+
+def test_empty_file(tmp_path):
+    p = str(tmp_path / "e.fastq")
+    write(p, b"", False)
+    got = []
+    process_fastq_file_in_chunks(p, 10, got.append)
+    assert got == [] and count_bases_in_fastq(p) == 0
