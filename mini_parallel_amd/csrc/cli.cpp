@@ -1,0 +1,761 @@
+// cli.cpp -- `rustseq_mini`, the reference CLI (smith_waterman/src/main.rs)
+// rebuilt over the MI355X scorer's C ABI (include/msw.h, include/msw_fastq.h).
+//
+// Flags of main.rs:11-46 are kept (-1/--seq1, -2/--seq2, -f/--files,
+// -c/--chunk-size (unused, as in the reference), -g/--gpu, -n/--num-files
+// (unused), -t/--test-wgs, --full-wgs), plus:
+//   --score-mode compat|sw   compat (default) = the kernel the reference launches
+//                            (smith_waterman.cl:11-71); sw = Smith-Waterman
+//   --gap-model linear|affine, --match/--mismatch/--gap-open/--gap-extend
+//   --reference FASTA        sw --full-wgs: read i is scored against
+//                            reference[pos : pos + window], pos from the
+//                            "pos=" tag of its FASTQ header
+//   --window N               window length (default 2 x read length)
+//   --num-gpus N             --full-wgs: lane files sharded over N GPUs
+//   --checkpoint-dir DIR     checkpoint_<run_id>.json written per file, resumed
+//   --json PATH              run record (benchmark.rs:17-34 fields + GCUPS)
+// Environment (.env loaded like dotenv, main.rs:50): WGS_DATA_DIR,
+// WGS_SAMPLE_ID, WGS_LANES, WGS_READS_PER_LANE (aligner.rs:184-195),
+// GPU_CHUNK_SIZE_READS (mandatory for chunked modes, aligner.rs:9-15),
+// WGS_RUN_ID (stable checkpoint id).
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "msw.h"
+#include "msw_fastq.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double ms_since(Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+[[noreturn]] void die(const std::string& msg) {
+    fflush(stdout);
+    fprintf(stderr, "%s\n", msg.c_str());
+    exit(1);
+}
+
+std::string env_or(const char* k, const std::string& d) {
+    const char* v = getenv(k);
+    return v ? std::string(v) : d;
+}
+
+// dotenv::dotenv().ok() (main.rs:50): KEY=VALUE lines of ./.env, existing
+// variables win, missing file is fine.
+void load_dotenv() {
+    std::ifstream f(".env");
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.empty() || line[0] == '#') continue;
+        const size_t eq = line.find('=');
+        if (eq == std::string::npos) continue;
+        std::string k = line.substr(0, eq), v = line.substr(eq + 1);
+        while (!k.empty() && isspace((unsigned char)k.back())) k.pop_back();
+        while (!v.empty() && isspace((unsigned char)v.front())) v.erase(v.begin());
+        if (v.size() >= 2 && (v.front() == '"' || v.front() == '\'') && v.back() == v.front())
+            v = v.substr(1, v.size() - 2);
+        setenv(k.c_str(), v.c_str(), 0);
+    }
+}
+
+// aligner.rs:9-15
+uint64_t get_chunk_size_reads() {
+    const char* v = getenv("GPU_CHUNK_SIZE_READS");
+    if (!v) die("error: GPU_CHUNK_SIZE_READS not set in .env file");
+    char* end = nullptr;
+    unsigned long long n = strtoull(v, &end, 10);
+    if (!*v || *end || n == 0) die(std::string("error: Invalid GPU_CHUNK_SIZE_READS value '") + v + "'");
+    return n;
+}
+
+struct Args {
+    std::string seq1, seq2;
+    bool has_seq1 = false, has_seq2 = false, files = false, gpu = false, test_wgs = false, full_wgs = false;
+    long chunk_size = 1, num_files = -1;
+    std::string score_mode = "compat", gap_model = "linear", reference, checkpoint_dir = ".", json;
+    int match = 2, mismatch = -1, gap_open = 3, gap_extend = -1, window = 0, num_gpus = 1;
+};
+
+void usage() {
+    printf(
+        "High-performance sequence alignment for genome-scale data (MI355X)\n\n"
+        "Usage: rustseq_mini [OPTIONS]\n\n"
+        "Options:\n"
+        "  -1, --seq1 <SEQ1>            first sequence or file path\n"
+        "  -2, --seq2 <SEQ2>            second sequence or file path\n"
+        "  -f, --files                  treat inputs as file paths instead of direct sequences\n"
+        "  -c, --chunk-size <N>         chunk size in MB (accepted, unused as in the reference)\n"
+        "  -g, --gpu                    use GPU acceleration if available\n"
+        "  -n, --num-files <N>          number of files (accepted, unused as in the reference)\n"
+        "  -t, --test-wgs               count bases of the first lane's files\n"
+        "      --full-wgs               process the full WGS dataset\n"
+        "      --score-mode <compat|sw> compat = reference kernel semantics (default), sw = Smith-Waterman\n"
+        "      --gap-model <linear|affine>\n"
+        "      --match N --mismatch N --gap-open N --gap-extend N\n"
+        "      --reference <FASTA>      reference genome for --full-wgs --score-mode sw\n"
+        "      --window N               window length (default 2 x read length)\n"
+        "      --num-gpus N             GPUs for --full-wgs\n"
+        "      --checkpoint-dir DIR     where checkpoint_<run_id>.json lives (default .)\n"
+        "      --json PATH              write a JSON run record\n"
+        "  -h, --help\n");
+}
+
+Args parse_args(int argc, char** argv) {
+    Args a;
+    auto need = [&](int& i) -> std::string {
+        if (i + 1 >= argc) die(std::string("error: a value is required for '") + argv[i] + "'");
+        return argv[++i];
+    };
+    for (int i = 1; i < argc; ++i) {
+        std::string s = argv[i];
+        std::string val;
+        const size_t eq = s.find('=');
+        if (s.rfind("--", 0) == 0 && eq != std::string::npos) { val = s.substr(eq + 1); s = s.substr(0, eq); }
+        auto v = [&]() { return val.empty() ? need(i) : val; };
+        if (s == "-1" || s == "--seq1") { a.seq1 = v(); a.has_seq1 = true; }
+        else if (s == "-2" || s == "--seq2") { a.seq2 = v(); a.has_seq2 = true; }
+        else if (s == "-f" || s == "--files") a.files = true;
+        else if (s == "-c" || s == "--chunk-size") a.chunk_size = atol(v().c_str());
+        else if (s == "-g" || s == "--gpu") a.gpu = true;
+        else if (s == "-n" || s == "--num-files") a.num_files = atol(v().c_str());
+        else if (s == "-t" || s == "--test-wgs") a.test_wgs = true;
+        else if (s == "--full-wgs") a.full_wgs = true;
+        else if (s == "--score-mode") a.score_mode = v();
+        else if (s == "--gap-model") a.gap_model = v();
+        else if (s == "--match") a.match = atoi(v().c_str());
+        else if (s == "--mismatch") a.mismatch = atoi(v().c_str());
+        else if (s == "--gap-open") a.gap_open = atoi(v().c_str());
+        else if (s == "--gap-extend") a.gap_extend = atoi(v().c_str());
+        else if (s == "--reference") a.reference = v();
+        else if (s == "--window") a.window = atoi(v().c_str());
+        else if (s == "--num-gpus") a.num_gpus = atoi(v().c_str());
+        else if (s == "--checkpoint-dir") a.checkpoint_dir = v();
+        else if (s == "--json") a.json = v();
+        else if (s == "-h" || s == "--help") { usage(); exit(0); }
+        else die("error: unexpected argument '" + s + "' found\n\nFor more information, try '--help'.");
+    }
+    if (a.score_mode != "compat" && a.score_mode != "sw") die("error: --score-mode must be compat or sw");
+    if (a.gap_model != "linear" && a.gap_model != "affine") die("error: --gap-model must be linear or affine");
+    if (a.gap_extend < 0) a.gap_extend = a.gap_model == "affine" ? 1 : 2;
+    return a;
+}
+
+msw_scoring_t scoring_of(const Args& a) {
+    msw_scoring_t sc;
+    sc.match = a.match;
+    sc.mismatch = a.mismatch;
+    sc.gap_open = a.gap_model == "affine" ? a.gap_open : 0;
+    sc.gap_extend = a.gap_extend;
+    sc.affine = a.gap_model == "affine";
+    sc.want_coords = 1;
+    return sc;
+}
+
+struct Device {
+    int ordinal;
+    std::string name;
+    double memory_gb;
+    uint32_t max_wg;
+};
+
+bool is_gpu_available() {
+    int n = 0;
+    return msw_device_count(&n) == MSW_OK && n > 0;
+}
+
+std::vector<Device> get_gpu_devices() {
+    std::vector<Device> out;
+    int n = 0;
+    if (msw_device_count(&n) != MSW_OK) return out;
+    for (int i = 0; i < n; ++i) {
+        msw_device_info_t info;
+        if (msw_device_info(i, &info) != MSW_OK) continue;
+        out.push_back({i, info.name, info.mem_bytes / 1073741824.0, info.max_wg});
+    }
+    return out;
+}
+
+struct Ctx {
+    msw_ctx* h = nullptr;
+    explicit Ctx(int ordinal) {
+        if (msw_ctx_create(ordinal, &h) != MSW_OK) die(std::string("GPU context error: ") + msw_last_error());
+    }
+    ~Ctx() { msw_ctx_destroy(h); }
+};
+
+// gpu_align (aligner.rs:410-532) through msw_align_compat.
+int32_t gpu_align(Ctx& ctx, const std::string& s1, const std::string& s2, const Device& dev, bool* ok,
+                  std::string* err) {
+    int32_t score = 0;
+    const uint32_t wg = std::min<uint32_t>(dev.max_wg, 1024);
+    const int rc = msw_align_compat(ctx.h, (const uint8_t*)s1.data(), s1.size(), (const uint8_t*)s2.data(),
+                                    s2.size(), wg, 1000000, &score);
+    *ok = rc == MSW_OK;
+    if (!*ok && err) *err = msw_last_error();
+    return score;
+}
+
+// A FASTQ file as chunks of concatenated sequences (the Vec<String> + concat
+// of aligner.rs:270 / :392-393).
+int for_each_fastq_chunk(const std::string& path, uint64_t chunk, const std::function<int(std::string&)>& fn,
+                         uint64_t* bases = nullptr, uint64_t* reads = nullptr) {
+    msw_fastq* fq = nullptr;
+    if (msw_fastq_open(path.c_str(), &fq) != MSW_OK) return -1;
+    constexpr uint32_t kStride = 4096;
+    std::vector<uint8_t> slab((size_t)std::min<uint64_t>(chunk, 65536) * kStride);
+    std::vector<uint16_t> lens(std::min<uint64_t>(chunk, 65536));
+    std::string cat;
+    uint64_t in_chunk = 0, nb = 0, nr = 0;
+    int rc = 0;
+    for (;;) {
+        uint64_t want = std::min<uint64_t>(chunk - in_chunk, lens.size()), got = 0;
+        rc = msw_fastq_next(fq, slab.data(), lens.data(), kStride, want, &got, nullptr);
+        if (rc) break;
+        for (uint64_t i = 0; i < got; ++i) {
+            cat.append((const char*)slab.data() + i * kStride, lens[i]);
+            nb += lens[i];
+        }
+        nr += got;
+        in_chunk += got;
+        if (got == 0 || in_chunk == chunk) {
+            if (in_chunk > 0) {
+                rc = fn(cat);
+                if (rc) break;
+            }
+            cat.clear();
+            in_chunk = 0;
+            if (got == 0) break;
+        }
+    }
+    msw_fastq_close(fq);
+    if (bases) *bases = nb;
+    if (reads) *reads = nr;
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Reference genome (FASTA) for sw mode.
+// ---------------------------------------------------------------------------
+std::string load_fasta(const std::string& path) {
+    std::ifstream f(path);
+    if (!f) die("error: cannot open reference " + path);
+    std::string line, seq;
+    while (std::getline(f, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        if (line.empty() || line[0] == '>') continue;
+        seq += line;
+    }
+    return seq;
+}
+
+// ---------------------------------------------------------------------------
+// Checkpoint / resume (aligner.rs:22-104 schema, with the bugs fixed: one
+// stable file name per run id, i64 scores, resume skips completed files).
+// ---------------------------------------------------------------------------
+struct FileCheckpoint {
+    std::string file_path;
+    size_t file_index = 0;
+    long long score = 0;
+    double processing_time_ms = 0;
+    unsigned long long total_bases = 0, total_reads = 0;
+    bool completed = false;
+};
+
+std::string json_escape(const std::string& s) {
+    std::string o;
+    for (char c : s) {
+        if (c == '"' || c == '\\') { o += '\\'; o += c; }
+        else if ((unsigned char)c < 0x20) { char b[8]; snprintf(b, sizeof(b), "\\u%04x", c); o += b; }
+        else o += c;
+    }
+    return o;
+}
+
+struct Checkpoint {
+    std::string run_id, path;
+    size_t total_files = 0;
+    std::map<size_t, FileCheckpoint> files;
+
+    void save() const {
+        std::ostringstream o;
+        size_t done = 0;
+        for (auto& kv : files) done += kv.second.completed;
+        o << "{\n  \"run_id\": \"" << json_escape(run_id) << "\",\n  \"files\": [";
+        bool first = true;
+        for (auto& kv : files) {
+            const FileCheckpoint& f = kv.second;
+            o << (first ? "\n" : ",\n") << "    {\"file_path\": \"" << json_escape(f.file_path)
+              << "\", \"file_index\": " << f.file_index << ", \"score\": " << f.score
+              << ", \"processing_time_ms\": " << f.processing_time_ms << ", \"total_bases\": " << f.total_bases
+              << ", \"total_reads\": " << f.total_reads << ", \"completed\": " << (f.completed ? "true" : "false")
+              << "}";
+            first = false;
+        }
+        o << "\n  ],\n  \"total_files\": " << total_files << ",\n  \"completed_files\": " << done << "\n}\n";
+        const std::string tmp = path + ".tmp";
+        {
+            std::ofstream f(tmp);
+            f << o.str();
+        }
+        rename(tmp.c_str(), path.c_str());  // atomic replace
+    }
+
+    // Minimal parser for the file this program writes.
+    bool load() {
+        std::ifstream f(path);
+        if (!f) return false;
+        std::stringstream ss;
+        ss << f.rdbuf();
+        const std::string s = ss.str();
+        size_t p = 0;
+        while ((p = s.find("{\"file_path\": \"", p)) != std::string::npos) {
+            FileCheckpoint c;
+            size_t q = s.find('"', p + 15);
+            c.file_path = s.substr(p + 15, q - (p + 15));
+            auto num = [&](const char* key) -> std::string {
+                size_t k = s.find(key, q);
+                if (k == std::string::npos) return "0";
+                k += strlen(key);
+                size_t e = s.find_first_of(",}", k);
+                return s.substr(k, e - k);
+            };
+            c.file_index = strtoull(num("\"file_index\": ").c_str(), nullptr, 10);
+            c.score = strtoll(num("\"score\": ").c_str(), nullptr, 10);
+            c.processing_time_ms = atof(num("\"processing_time_ms\": ").c_str());
+            c.total_bases = strtoull(num("\"total_bases\": ").c_str(), nullptr, 10);
+            c.total_reads = strtoull(num("\"total_reads\": ").c_str(), nullptr, 10);
+            c.completed = num("\"completed\": ").find("true") != std::string::npos;
+            files[c.file_index] = c;
+            p = q;
+        }
+        return true;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// --full-wgs driver: reader threads fill read slabs, a bounded queue hands
+// chunks to one host thread per GPU (own msw_ctx), results are summed per file.
+// ---------------------------------------------------------------------------
+struct Chunk {
+    size_t file_index;
+    std::vector<uint8_t> reads;   // n x kReadStride
+    std::vector<uint16_t> rlen;
+    std::vector<int64_t> pos;
+    uint64_t n = 0;
+    bool last = false;            // last chunk of its file
+};
+
+constexpr uint32_t kReadStride = 256;
+
+struct FileState {
+    std::string path;
+    std::atomic<long long> score{0};
+    std::atomic<unsigned long long> bases{0}, reads{0};
+    std::atomic<int> outstanding{0};
+    std::atomic<bool> reader_done{false}, failed{false}, finished{false};
+    Clock::time_point t0;
+    double ms = 0;
+    std::string error;
+};
+
+class ChunkQueue {
+   public:
+    explicit ChunkQueue(size_t cap) : cap_(cap) {}
+    void push(std::unique_ptr<Chunk> c) {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_space_.wait(lk, [&] { return q_.size() < cap_; });
+        q_.push_back(std::move(c));
+        cv_item_.notify_one();
+    }
+    std::unique_ptr<Chunk> pop() {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_item_.wait(lk, [&] { return !q_.empty() || closed_; });
+        if (q_.empty()) return nullptr;
+        auto c = std::move(q_.front());
+        q_.pop_front();
+        cv_space_.notify_one();
+        return c;
+    }
+    void close() {
+        std::lock_guard<std::mutex> lk(m_);
+        closed_ = true;
+        cv_item_.notify_all();
+    }
+
+   private:
+    std::mutex m_;
+    std::condition_variable cv_item_, cv_space_;
+    std::deque<std::unique_ptr<Chunk>> q_;
+    size_t cap_;
+    bool closed_ = false;
+};
+
+struct WgsReport {
+    std::vector<FileCheckpoint> results;
+    double wall_ms = 0;
+    unsigned long long cells = 0;
+};
+
+WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const std::vector<std::string>& files,
+                       Checkpoint& ckpt) {
+    const uint64_t chunk = get_chunk_size_reads();
+    const bool sw = a.score_mode == "sw";
+    std::string genome;
+    if (sw) {
+        if (a.reference.empty()) die("error: --score-mode sw with --full-wgs needs --reference <FASTA>");
+        genome = load_fasta(a.reference);
+        printf("Loaded reference: %zu bases\n", genome.size());
+    }
+    const int ngpu = std::max(1, std::min<int>(a.num_gpus, (int)devices.size()));
+    std::vector<std::unique_ptr<FileState>> st(files.size());
+    std::vector<size_t> todo;
+    for (size_t i = 0; i < files.size(); ++i) {
+        st[i].reset(new FileState());
+        st[i]->path = files[i];
+        auto it = ckpt.files.find(i);
+        if (it != ckpt.files.end() && it->second.completed && it->second.file_path == files[i]) {
+            printf("  Skipping completed file %zu/%zu: %s (score %lld)\n", i + 1, files.size(), files[i].c_str(),
+                   it->second.score);
+        } else {
+            todo.push_back(i);
+        }
+    }
+    ChunkQueue queue(2 * (size_t)ngpu + 2);
+    std::mutex ck_mu;
+    std::atomic<unsigned long long> cells{0};
+    const auto t_all = Clock::now();
+
+    auto finish_file = [&](size_t fi) {
+        FileState& f = *st[fi];
+        if (f.finished.exchange(true)) return;  // exactly once (reader or GPU thread)
+        f.ms = ms_since(f.t0);
+        FileCheckpoint c;
+        c.file_path = f.path;
+        c.file_index = fi;
+        c.score = f.score.load();
+        c.processing_time_ms = f.ms;
+        c.total_bases = f.bases.load();
+        c.total_reads = f.reads.load();
+        c.completed = !f.failed.load();
+        std::lock_guard<std::mutex> lk(ck_mu);
+        ckpt.files[fi] = c;
+        ckpt.save();
+        printf("  File %zu done: %s score=%lld reads=%llu bases=%llu time=%.2fs%s\n", fi + 1, f.path.c_str(),
+               c.score, c.total_reads, c.total_bases, f.ms / 1000.0, c.completed ? "" : " (FAILED)");
+        fflush(stdout);
+    };
+
+    // Readers: as many concurrent files as GPUs x 2 (gzip is single-stream).
+    std::atomic<size_t> next_file{0};
+    const int nreaders = std::max(1, std::min<int>((int)todo.size(), 2 * ngpu));
+    std::vector<std::thread> readers;
+    std::atomic<int> readers_left{nreaders};
+    for (int r = 0; r < nreaders; ++r) {
+        readers.emplace_back([&]() {
+            for (;;) {
+                const size_t k = next_file.fetch_add(1);
+                if (k >= todo.size()) break;
+                const size_t fi = todo[k];
+                FileState& f = *st[fi];
+                f.t0 = Clock::now();
+                printf("  Processing file %zu/%zu: %s\n", fi + 1, files.size(), f.path.c_str());
+                fflush(stdout);
+                msw_fastq* fq = nullptr;
+                if (msw_fastq_open(f.path.c_str(), &fq) != MSW_OK) {
+                    f.error = msw_last_error();
+                    f.failed = true;
+                    f.reader_done = true;
+                    if (f.outstanding.load() == 0) finish_file(fi);
+                    continue;
+                }
+                for (;;) {
+                    std::unique_ptr<Chunk> c(new Chunk());
+                    c->file_index = fi;
+                    c->reads.resize(chunk * kReadStride);
+                    c->rlen.resize(chunk);
+                    c->pos.resize(chunk);
+                    if (msw_fastq_next(fq, c->reads.data(), c->rlen.data(), kReadStride, chunk, &c->n,
+                                       c->pos.data()) != MSW_OK) {
+                        f.error = msw_last_error();
+                        fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
+                        f.failed = true;
+                        break;
+                    }
+                    if (c->n == 0) break;
+                    f.outstanding.fetch_add(1);
+                    queue.push(std::move(c));
+                }
+                msw_fastq_close(fq);
+                f.reader_done = true;
+                // A file with no chunks in flight is finished here; otherwise by the GPU thread.
+                if (f.outstanding.load() == 0) finish_file(fi);
+            }
+            if (readers_left.fetch_sub(1) == 1) queue.close();
+        });
+    }
+
+    std::vector<std::thread> workers;
+    for (int g = 0; g < ngpu; ++g) {
+        workers.emplace_back([&, g]() {
+            Ctx ctx(devices[g].ordinal);
+            const msw_scoring_t sc = scoring_of(a);
+            std::vector<uint8_t> wins;
+            std::vector<uint16_t> wlen;
+            std::vector<int32_t> score;
+            std::vector<int16_t> ei, ej;
+            for (;;) {
+                std::unique_ptr<Chunk> c = queue.pop();
+                if (!c) break;
+                FileState& f = *st[c->file_index];
+                long long chunk_score = 0;
+                unsigned long long nb = 0;
+                for (uint64_t i = 0; i < c->n; ++i) nb += c->rlen[i];
+                if (sw) {
+                    // window = reference[pos : pos + W] (W = --window or 2 x read length)
+                    const uint32_t ws = 512;
+                    wins.assign(c->n * ws, 0);
+                    wlen.assign(c->n, 0);
+                    score.assign(c->n, 0);
+                    ei.assign(c->n, 0);
+                    ej.assign(c->n, 0);
+                    unsigned long long cc = 0;
+                    for (uint64_t i = 0; i < c->n; ++i) {
+                        const int64_t p = c->pos[i];
+                        uint32_t w = a.window > 0 ? (uint32_t)a.window : 2u * c->rlen[i];
+                        w = std::min<uint32_t>(w, ws);
+                        if (p < 0 || (uint64_t)p >= genome.size()) { wlen[i] = 0; continue; }
+                        w = (uint32_t)std::min<uint64_t>(w, genome.size() - (uint64_t)p);
+                        memcpy(wins.data() + i * ws, genome.data() + p, w);
+                        wlen[i] = (uint16_t)w;
+                        cc += (unsigned long long)w * c->rlen[i];
+                    }
+                    msw_batch_t b{c->reads.data(), wins.data(), c->rlen.data(), wlen.data(), kReadStride, ws, c->n};
+                    msw_out_t o{score.data(), ei.data(), ej.data()};
+                    if (msw_align_batch(ctx.h, &sc, &b, &o, 0) != MSW_OK) {
+                        fprintf(stderr, "  GPU %d alignment error: %s\n", g, msw_last_error());
+                        f.failed = true;
+                    } else {
+                        for (uint64_t i = 0; i < c->n; ++i) chunk_score += score[i];
+                        cells += cc;
+                    }
+                } else {
+                    // compat: chunk concat self-aligned (aligner.rs:269-276, :365-373)
+                    std::string cat;
+                    cat.reserve(nb);
+                    for (uint64_t i = 0; i < c->n; ++i) cat.append((const char*)c->reads.data() + i * kReadStride, c->rlen[i]);
+                    if (cat.size() >= 1000) {
+                        int32_t s = 0;
+                        if (msw_align_compat(ctx.h, (const uint8_t*)cat.data(), cat.size(), (const uint8_t*)cat.data(),
+                                             cat.size(), std::min<uint32_t>(devices[g].max_wg, 1024), 1000000,
+                                             &s) != MSW_OK) {
+                            fprintf(stderr, "  GPU %d alignment error: %s\n", g, msw_last_error());
+                            f.failed = true;
+                        }
+                        chunk_score = s;
+                    }
+                }
+                f.score += chunk_score;
+                f.bases += nb;
+                f.reads += c->n;
+                if (f.outstanding.fetch_sub(1) == 1 && f.reader_done.load()) finish_file(c->file_index);
+            }
+        });
+    }
+    for (auto& t : readers) t.join();
+    for (auto& t : workers) t.join();
+    for (size_t fi : todo) finish_file(fi);  // no-op for files already finished
+    WgsReport rep;
+    rep.wall_ms = ms_since(t_all);
+    rep.cells = cells.load();
+    for (size_t i = 0; i < files.size(); ++i)
+        if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
+    return rep;
+}
+
+std::string stable_run_id(const std::string& dir, const std::string& sample, const Args& a) {
+    const char* v = getenv("WGS_RUN_ID");
+    if (v && *v) return v;
+    // FNV-1a over the inputs that define the run: same dataset + mode -> same id.
+    std::string key = dir + "|" + sample + "|" + a.score_mode + "|" + a.gap_model + "|" + a.reference + "|" +
+                      env_or("GPU_CHUNK_SIZE_READS", "");
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : key) { h ^= c; h *= 1099511628211ull; }
+    char buf[32];
+    snprintf(buf, sizeof(buf), "wgs_%016llx", (unsigned long long)h);
+    return buf;
+}
+
+void write_json(const std::string& path, const std::string& body) {
+    if (path.empty()) return;
+    std::ofstream f(path);
+    f << body;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    load_dotenv();
+    const Args a = parse_args(argc, argv);
+    const auto devices = get_gpu_devices();
+    printf("Detecting system information...\n");
+    for (const auto& d : devices) printf("  GPU %d: %s (%.1f GB)\n", d.ordinal, d.name.c_str(), d.memory_gb);
+    if (devices.empty()) printf("  No GPU detected\n");
+
+    if (a.full_wgs) {
+        printf("Processing FULL WGS dataset...\n");
+        if (!a.gpu || !is_gpu_available()) die("error: gpu acceleration is required for full WGS processing");
+        const std::string dir = env_or("WGS_DATA_DIR", "/path/to/wgs/data");
+        const std::string sample = env_or("WGS_SAMPLE_ID", "SAMPLE_ID");
+        const int lanes = atoi(env_or("WGS_LANES", "8").c_str()) > 0 ? atoi(env_or("WGS_LANES", "8").c_str()) : 8;
+        const int rpl = atoi(env_or("WGS_READS_PER_LANE", "2").c_str()) > 0
+                            ? atoi(env_or("WGS_READS_PER_LANE", "2").c_str()) : 2;
+        std::vector<std::string> files;
+        for (int lane = 1; lane <= lanes; ++lane)
+            for (int r = 1; r <= rpl; ++r) {
+                char name[512];
+                snprintf(name, sizeof(name), "%s/%s_L%03d_R%d_001.fastq.gz", dir.c_str(), sample.c_str(), lane, r);
+                files.push_back(name);
+            }
+        Checkpoint ck;
+        ck.run_id = stable_run_id(dir, sample, a);
+        ck.path = a.checkpoint_dir + "/checkpoint_" + ck.run_id + ".json";
+        ck.total_files = files.size();
+        if (ck.load()) printf("Resuming run %s from %s\n", ck.run_id.c_str(), ck.path.c_str());
+        const WgsReport rep = run_full_wgs(a, devices, files, ck);
+        long long total = 0;
+        unsigned long long reads = 0, bases = 0;
+        bool all_ok = true;
+        printf("\nFULL WGS PROCESSING COMPLETE\n==========================================\n");
+        printf("Total files processed: %zu\n", rep.results.size());
+        for (const auto& r : rep.results) {
+            printf("File %zu: Score=%lld, Time=%.2fs\n", r.file_index + 1, r.score, r.processing_time_ms / 1000.0);
+            total += r.score;
+            reads += r.total_reads;
+            bases += r.total_bases;
+            all_ok = all_ok && r.completed;
+        }
+        printf("Total reads: %llu, total bases: %llu, total score: %lld\n", reads, bases, total);
+        printf("Wall time: %.2f s", rep.wall_ms / 1000.0);
+        if (rep.cells) printf(", %.1f GCUPS end-to-end", rep.cells / (rep.wall_ms * 1e6));
+        printf("\n");
+        std::ostringstream j;
+        j << "{\"mode\": \"full_wgs\", \"score_mode\": \"" << a.score_mode << "\", \"run_id\": \"" << ck.run_id
+          << "\", \"num_gpus\": " << std::max(1, std::min<int>(a.num_gpus, (int)devices.size()))
+          << ", \"total_files\": " << files.size() << ", \"total_reads\": " << reads << ", \"total_bases\": " << bases
+          << ", \"total_score\": " << total << ", \"wall_ms\": " << rep.wall_ms << ", \"cells\": " << rep.cells
+          << ", \"gcups_end_to_end\": " << (rep.cells ? rep.cells / (rep.wall_ms * 1e6) : 0.0)
+          << ", \"reads_per_second\": " << (reads / std::max(rep.wall_ms / 1000.0, 1e-9))
+          << ", \"host_cores\": " << std::thread::hardware_concurrency() << "}\n";
+        write_json(a.json, j.str());
+        return all_ok ? 0 : 1;
+    }
+
+    if (a.test_wgs) {
+        printf("Testing WGS file reading from configured directory...\n");
+        const std::string dir = env_or("WGS_DATA_DIR", "/path/to/wgs/data");
+        const std::string sample = env_or("WGS_SAMPLE_ID", "SAMPLE_ID");
+        for (const char* rr : {"R1", "R2"}) {
+            const std::string file = sample + "_L001_" + rr + "_001.fastq.gz";
+            const std::string full = dir + "/" + file;
+            printf("Testing: %s\n", full.c_str());
+            uint64_t bases = 0, reads = 0;
+            get_chunk_size_reads();  // count_bases_in_fastq needs it (aligner.rs:538)
+            if (msw_fastq_count_bases(full.c_str(), &bases, &reads) == MSW_OK)
+                printf("✅ Successfully counted %llu bases in %s\n", (unsigned long long)bases, file.c_str());
+            else
+                printf("❌ Error counting bases in %s: %s\n", file.c_str(), msw_last_error());
+        }
+        return 0;
+    }
+
+    if (!a.has_seq1) die("--seq1 is required when not in test mode");
+    if (!a.has_seq2) die("--seq2 is required when not in test mode");
+    if (!a.gpu || !is_gpu_available()) die("error: gpu acceleration is required and no compatible gpu was found");
+    printf("GPU acceleration enabled\n");
+    for (const auto& d : devices) printf("  Found GPU: %s (%g GB)\n", d.name.c_str(), d.memory_gb);
+    const Device& dev = devices[0];
+    Ctx ctx(dev.ordinal);
+
+    if (a.files) {
+        // gpu_align_pair (aligner.rs:376-407)
+        uint64_t b1 = 0, b2 = 0, r = 0;
+        const uint64_t chunk = get_chunk_size_reads();
+        if (msw_fastq_count_bases(a.seq1.c_str(), &b1, &r) || msw_fastq_count_bases(a.seq2.c_str(), &b2, &r)) {
+            fprintf(stderr, "GPU alignment error: %s\n", msw_last_error());
+            return 1;
+        }
+        printf("Loaded %llu bases from %s\n", (unsigned long long)b1, a.seq1.c_str());
+        printf("Loaded %llu bases from %s\n", (unsigned long long)b2, a.seq2.c_str());
+        const auto t0 = Clock::now();
+        // File 2's chunks are cached (the reference re-decompresses file 2 once
+        // per chunk of file 1, aligner.rs:390-398; the sum is identical).
+        std::vector<std::string> chunks2;
+        for_each_fastq_chunk(a.seq2, chunk, [&](std::string& c) { chunks2.push_back(c); return 0; });
+        int32_t total = 0;  // i32 sum, wrapping like a release build
+        std::string err;
+        const int rc = for_each_fastq_chunk(a.seq1, chunk, [&](std::string& c1) {
+            for (const auto& c2 : chunks2) {
+                bool ok = false;
+                const int32_t s = gpu_align(ctx, c1, c2, dev, &ok, &err);
+                if (!ok) return 1;
+                total = (int32_t)((uint32_t)total + (uint32_t)s);
+            }
+            return 0;
+        });
+        if (rc) {
+            fprintf(stderr, "GPU alignment error: %s\n", err.empty() ? msw_last_error() : err.c_str());
+            return 1;
+        }
+        printf("GPU Alignment Result:\n  Score: %d\n  Processing time: %.2f ms\n  GPU device: %s\n", total,
+               (double)(long long)ms_since(t0), dev.name.c_str());
+        return 0;
+    }
+
+    if (a.score_mode == "sw") {
+        msw_scoring_t sc = scoring_of(a);
+        const size_t rs = std::max<size_t>(16, (a.seq1.size() + 15) / 16 * 16);
+        const size_t ws = std::max<size_t>(16, (a.seq2.size() + 15) / 16 * 16);
+        std::vector<uint8_t> r(rs, 0), w(ws, 0);
+        memcpy(r.data(), a.seq1.data(), a.seq1.size());
+        memcpy(w.data(), a.seq2.data(), a.seq2.size());
+        uint16_t rl = (uint16_t)a.seq1.size(), wl = (uint16_t)a.seq2.size();
+        int32_t score = 0;
+        int16_t ei = -1, ej = -1;
+        msw_batch_t b{r.data(), w.data(), &rl, &wl, (uint32_t)rs, (uint32_t)ws, 1};
+        msw_out_t o{&score, &ei, &ej};
+        if (msw_align_batch(ctx.h, &sc, &b, &o, 0) != MSW_OK) {
+            fprintf(stderr, "GPU alignment error: %s\n", msw_last_error());
+            return 1;
+        }
+        printf("GPU Alignment score: %d\n", score);
+        printf("Best cell: read %d, window %d\n", ei, ej);
+        return 0;
+    }
+    bool ok = false;
+    std::string err;
+    const int32_t score = gpu_align(ctx, a.seq1, a.seq2, dev, &ok, &err);
+    if (!ok) {
+        fprintf(stderr, "GPU alignment error: %s\n", err.c_str());
+        return 1;
+    }
+    printf("GPU Alignment score: %d\n", score);
+    return 0;
+}

@@ -105,3 +105,56 @@ def config_batch(k: int, n_pairs: int = 0, seed_offset: int = 0) -> PairBatch:
         return make_pairs(n_pairs or 100_000, (75, 250), 2.0, seed=seed, read_stride=256,
                           win_stride=512)
     raise ValueError(f"unknown config {k}")
+
+
+def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_per_lane: int = 2,
+                      reads_per_file: int = 1000, read_len: int = 150, win_factor: float = 2.0,
+                      seed: int = 1004, genome_bases: int = 1 << 20) -> dict:
+    """Config-4-shaped dataset: lane files {sample}_L{lane:03}_R{r}_001.fastq.gz
+    (aligner.rs:198-204 naming) whose headers carry "pos=<window start>", and
+    the reference genome as reference.fa.  Returns paths and the pair batches
+    (reads, windows) so tests can score them with the oracle."""
+    import gzip
+    import os
+    os.makedirs(out_dir, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    g = genome(genome_bases, rng)
+    with open(os.path.join(out_dir, "reference.fa"), "w") as f:
+        f.write(">synthetic seed=%d\n" % seed)
+        s = g.tobytes().decode()
+        for k in range(0, len(s), 80):
+            f.write(s[k:k + 80] + "\n")
+    files, batches = [], []
+    k = 0
+    for lane in range(1, lanes + 1):
+        for r in range(1, reads_per_lane + 1):
+            b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_bases=genome_bases,
+                           read_stride=(read_len + 16 + 15) // 16 * 16)
+            # windows must come from THIS genome: re-cut them at b.pos (pos of
+            # unrelated reads is drawn too, so every read has a window)
+            pos = rng.integers(0, genome_bases - int(b.win_len.max()), b.n_pairs)
+            pos = np.where(b.pos >= 0, np.minimum(b.pos, genome_bases - int(b.win_len.max())), pos)
+            wins = np.zeros_like(b.wins)
+            for i in range(b.n_pairs):
+                n = int(b.win_len[i])
+                wins[i, :n] = g[pos[i]:pos[i] + n]
+            # reads: sample from this genome at the window centre, mutate like make_pairs
+            reads = np.zeros_like(b.reads)
+            for i in range(b.n_pairs):
+                m = int(b.read_len[i])
+                off = pos[i] + (int(b.win_len[i]) - m) // 2
+                src = g[off:off + m].copy() if b.pos[i] >= 0 else b.reads[i, :m]
+                subs = rng.random(m) < 0.01
+                src[subs] = ACGT[(np.searchsorted(ACGT, src[subs]) + rng.integers(1, 4, int(subs.sum()))) % 4]
+                reads[i, :m] = src
+            name = os.path.join(out_dir, "%s_L%03d_R%d_001.fastq.gz" % (sample, lane, r))
+            with gzip.open(name, "wb", compresslevel=1) as f:
+                for i in range(b.n_pairs):
+                    m = int(b.read_len[i])
+                    f.write(b"@%s:%d:%d pos=%d\n" % (sample.encode(), lane, i, int(pos[i])))
+                    f.write(reads[i, :m].tobytes() + b"\n+\n" + b"I" * m + b"\n")
+            files.append(name)
+            batches.append(PairBatch(reads, b.read_len.copy(), wins, b.win_len.copy(), pos))
+            k += 1
+    return {"files": files, "reference": os.path.join(out_dir, "reference.fa"), "batches": batches,
+            "sample": sample, "lanes": lanes, "reads_per_lane": reads_per_lane}

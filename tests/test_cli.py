@@ -1,0 +1,146 @@
+"""rustseq_mini (C++ CLI over the C ABI): flag surface of main.rs:11-46 and the
+pair / --files / --test-wgs / --full-wgs modes against the oracle."""
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini")
+
+
+def run(args, env=None, cwd=None, timeout=600):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([CLI] + args, capture_output=True, text=True, env=e, cwd=cwd, timeout=timeout)
+
+
+def test_cli_built():
+    assert os.access(CLI, os.X_OK), "rustseq_mini not built (__graft_entry__.build())"
+
+
+def test_help_lists_reference_flags():
+    out = run(["--help"]).stdout
+    for flag in ["--seq1", "--seq2", "--files", "--chunk-size", "--gpu", "--num-files", "--test-wgs", "--full-wgs"]:
+        assert flag in out
+
+
+def test_requires_gpu_flag(tmp_path):
+    # main.rs:160-163: no --gpu -> error + exit 1 (no CPU path)
+    r = run(["-1", "ACGT", "-2", "ACGT"], cwd=tmp_path)
+    assert r.returncode == 1
+    assert "gpu acceleration is required" in r.stderr
+
+
+def test_full_wgs_requires_gpu_flag(tmp_path):
+    r = run(["--full-wgs"], cwd=tmp_path)
+    assert r.returncode == 1 and "required for full WGS" in r.stderr
+
+
+def test_unknown_flag(tmp_path):
+    r = run(["--bogus"], cwd=tmp_path)
+    assert r.returncode == 1 and "unexpected argument" in r.stderr
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present")
+def test_no_gpu_with_flag(tmp_path):
+    r = run(["-1", "ACGT", "-2", "ACGT", "--gpu"], cwd=tmp_path)
+    assert r.returncode == 1 and "no compatible gpu" in r.stderr
+
+
+# ---------------------------------------------------------------------------
+# GPU
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_pair_compat(tmp_path):
+    r = run(["-1", "ACGTACGT", "-2", "ACGTACGT", "--gpu"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "GPU Alignment score: 2" in r.stdout
+    r = run(["--seq1", "AAAA", "--seq2", "CCCC", "-g"], cwd=tmp_path)
+    assert "GPU Alignment score: 0" in r.stdout
+
+
+@pytest.mark.gpu
+def test_pair_sw(tmp_path):
+    r = run(["-1", "ACGTACGT", "-2", "ACGACGT", "--gpu", "--score-mode", "sw"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "GPU Alignment score: 12" in r.stdout and "read 7, window 6" in r.stdout
+
+
+def _fastq(path, seqs):
+    with open(path, "w") as f:
+        for i, s in enumerate(seqs):
+            f.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
+
+
+@pytest.mark.gpu
+def test_files_mode_compat(tmp_path, oracle):
+    rng = np.random.default_rng(5)
+    alpha = np.frombuffer(b"ACGT", np.uint8)
+    s1 = [bytes(rng.choice(alpha, 150)).decode() for _ in range(25)]
+    s2 = [bytes(rng.choice(alpha, 150)).decode() for _ in range(17)]
+    s2[3] = s1[0]
+    _fastq(tmp_path / "a.fastq", s1)
+    _fastq(tmp_path / "b.fastq", s2)
+    r = run(["-f", "-1", "a.fastq", "-2", "b.fastq", "--gpu"], env={"GPU_CHUNK_SIZE_READS": "10"}, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    want = 0
+    c1 = ["".join(s1[i:i + 10]) for i in range(0, len(s1), 10)]
+    c2 = ["".join(s2[i:i + 10]) for i in range(0, len(s2), 10)]
+    for a in c1:
+        for b in c2:
+            want += oracle.compat_align(a.encode(), b.encode(), 1024)
+    assert f"Score: {want}" in r.stdout
+    assert f"Loaded {150 * 25} bases from a.fastq" in r.stdout
+
+
+@pytest.mark.gpu
+def test_full_wgs_sw_and_resume(tmp_path, oracle):
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=2, reads_per_lane=2, reads_per_file=1500)
+    env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "2",
+           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "700", "WGS_RUN_ID": "t1"}
+    args = ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
+            "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json")]
+    r = run(args, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = 0
+    per_file = []
+    for b in ds["batches"]:
+        s, _, _ = oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=8)
+        per_file.append(int(s.astype(np.int64).sum()))
+        want += per_file[-1]
+    rec = json.load(open(tmp_path / "rec.json"))
+    assert rec["total_score"] == want and rec["total_reads"] == 6000
+    ck = json.load(open(tmp_path / "checkpoint_t1.json"))
+    assert ck["completed_files"] == 4
+    assert [f["score"] for f in sorted(ck["files"], key=lambda f: f["file_index"])] == per_file
+    # resume: every file is skipped, totals unchanged
+    r2 = run(args, env=env, cwd=tmp_path)
+    assert r2.returncode == 0 and r2.stdout.count("Skipping completed file") == 4
+    assert json.load(open(tmp_path / "rec.json"))["total_score"] == want
+
+
+@pytest.mark.gpu
+def test_full_wgs_compat_and_test_wgs(tmp_path):
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=1, reads_per_lane=2, reads_per_file=95)
+    env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "1",
+           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "10", "WGS_RUN_ID": "t2"}
+    r = run(["--full-wgs", "--gpu", "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "c.json")],
+            env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    # each chunk self-aligned: 2 when it has >= 1000 bases (aligner.rs:365-373)
+    want = 0
+    for b in ds["batches"]:
+        lens = b.read_len.astype(int)
+        for k in range(0, len(lens), 10):
+            want += 2 if lens[k:k + 10].sum() >= 1000 else 0
+    assert json.load(open(tmp_path / "c.json"))["total_score"] == want
+    r = run(["--test-wgs"], env=env, cwd=tmp_path)
+    assert r.returncode == 0
+    got = [int(x) for x in re.findall(r"Successfully counted (\d+) bases", r.stdout)]
+    assert got == [int(b.read_len.astype(int).sum()) for b in ds["batches"][:2]]
