@@ -19,10 +19,11 @@ constexpr int kMaxReadLen = 256;       // KR <= 16
 constexpr int kMaxWinLen = 4096;
 constexpr int kLead = 32;              // sentinel words in front of each window stream
 
-// u32 words per lane-group stream: kLead + (max_win + 31) steps + 1 lookahead,
+// u32 words per lane-group stream: kLead + (max_win + 31) steps rounded to even
+// + 2 lookahead,
 // rounded so that the four groups of a wave start 16 banks apart (== 16 mod 32).
 inline uint32_t stream_stride(uint32_t max_win_len) {
-    uint32_t words = kLead + max_win_len + 2 * kGroupLanes;
+    uint32_t words = kLead + max_win_len + 2 * kGroupLanes + 3;
     words = (words + 31u) & ~31u;
     return words + 16u;
 }

@@ -335,7 +335,8 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
     const int g = lane >> 4, lg = lane & 15;
     const PairMeta q = load_meta<SPLIT>(p, g, block);
     const int skew = SPLIT ? 2 * (kGroupLanes - 1) + 1 : kGroupLanes - 1;
-    const int steps = __builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + skew;
+    // wavefront steps, rounded up to even for the two-step unrolled loop
+    const int steps = (__builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + skew + 1) & ~1;
     uint32_t* stream = lds + g * p.lds_stride;
     stage_window<SPLIT>(p, q, stream, steps, lg);
     uint32_t rc[KR];
@@ -343,25 +344,38 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
     __syncthreads();
 
     const uint32_t match2 = p.match2, delta2 = p.delta2, ext2 = p.gap2, oe2 = p.open_ext2;
-    uint32_t E[KR], G[AFFINE ? KR : 1], DG[KR];
+    uint32_t E[KR], G[AFFINE ? KR : 1];
     uint32_t key_a[COORDS ? KR : 1], key_b[COORDS ? KR : 1];
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
         E[r] = 0u;
-        DG[r] = match2;
         if constexpr (AFFINE) G[r] = 0u;
         if constexpr (COORDS) { key_a[r] = 0u; key_b[r] = 0u; }
     }
-    uint32_t f_bot = 0u, h_bot = 0u, d_up_prev = match2;
+    uint32_t f_bot = 0u, h_bot = 0u;
     uint32_t best = 0u;
     // lane reads column t - lg (pairs) / t - 2lg (split) at stream index kLead + that
     const uint32_t* wp = stream + (kLead - (SPLIT ? 2 * lg : lg));
     const uint32_t nj_lane = (uint32_t)(0xFFFF + (SPLIT ? 2 * lg : lg));
 
-    uint32_t w_next = wp[0];  // one step of LDS lookahead
-    for (int t = 0; t < steps; ++t) {
-        const uint32_t w = w_next;
-        w_next = wp[t + 1];
+    // Software pipeline: t1 (the diagonal term) of step t+1 is formed inside
+    // step t's row chain, as soon as the H it needs is known, so each link of
+    // the dependent max3 -> sat-sub chain has independent work beside it
+    // (waves issue in order; a lone wave otherwise stalls on every link).
+    uint32_t t1a[KR], t1b[KR];
+    {
+        const uint32_t w0 = wp[0];
+#pragma unroll
+        for (int r = 0; r < KR; ++r) t1a[r] = pk_satsub(match2, pk_min(rc[r] ^ w0, delta2));
+    }
+    uint32_t w_next = wp[1];  // one step of LDS lookahead
+
+    // One wavefront step: consumes t1 (this step's diagonal terms), produces
+    // t1n (the next step's).  Called with alternating buffers so the hand-over
+    // needs no register copies.
+    auto step = [&](int t, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR]) __attribute__((always_inline)) {
+        const uint32_t w = w_next;  // window codes of step t + 1
+        w_next = wp[t + 2];
         const uint32_t d_up = add_nc(from_above<SPLIT>(h_bot), match2);
         uint32_t up;    // linear: E of the row above; affine: F of the row above
         uint32_t g_up;  // affine: G of the row above
@@ -372,10 +386,10 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
             up = from_above<SPLIT>(E[KR - 1]);
             g_up = 0u;
         }
-        DG[0] = d_up_prev;
-        uint32_t t1[KR];
+        uint32_t a_n[KR];
 #pragma unroll
-        for (int r = 0; r < KR; ++r) t1[r] = pk_satsub(DG[r], pk_min(rc[r] ^ w, delta2));
+        for (int r = 0; r < KR; ++r) a_n[r] = pk_min(rc[r] ^ w, delta2);
+        t1n[0] = pk_satsub(d_up, a_n[0]);  // row 0's diagonal next step: the lane above's H now
         const uint32_t nj_a = (nj_lane - (uint32_t)t) & 0xFFFFu;
         const uint32_t nj_b = SPLIT ? ((nj_lane + 1u - (uint32_t)t) & 0xFFFFu) : nj_a;
         uint32_t hprev = 0u;
@@ -392,7 +406,7 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
                 h = pk_max3(t1[r], E[r], up);
                 up = E[r] = pk_satsub(h, ext2);
             }
-            if (r + 1 < KR) DG[r + 1] = add_nc(h, match2);
+            if (r + 1 < KR) t1n[r + 1] = pk_satsub(add_nc(h, match2), a_n[r + 1]);
             else h_bot = h;
             if constexpr (COORDS) {
                 key_a[r] = max(key_a[r], (h << 16) | nj_a);
@@ -404,7 +418,12 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
             }
         }
         if constexpr (AFFINE) f_bot = up;
-        d_up_prev = d_up;
+    };
+    // Step count rounded up to even: the extra step scores sentinel columns,
+    // which never reach a real cell's score.
+    for (int t = 0; t < steps; t += 2) {
+        step(t, t1a, t1b);
+        step(t + 1, t1b, t1a);
     }
 
     if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, key_a, key_b);
