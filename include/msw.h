@@ -21,8 +21,8 @@
  *    window) of the best cell, smallest i then smallest j on ties; (-1,-1)
  *    when the score is 0 or the pair is empty.
  *  - Supported by the GPU kernels: read length <= 256, window length <= 4096,
- *    1 <= match <= 64, mismatch in [match-64, match], gaps >= 0 and
- *    match * (min(read,window)+1) < 31744.  Anything else -> MSW_E_RANGE.
+ *    1 <= match <= 64, match - 64 <= mismatch <= 0, 0 <= gap_extend <= 1024,
+ *    0 <= gap_open <= 30000.  Anything else -> MSW_E_RANGE.
  *    There is no CPU fallback: without a usable GPU every call fails.
  */
 #ifndef MSW_H

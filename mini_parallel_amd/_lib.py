@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmsw.so")
+# MSW_LIB_PATH lets A/B tooling (tools/sweep.py) load another in-tree build.
+LIB_PATH = os.environ.get("MSW_LIB_PATH") or os.path.join(_HERE, "libmsw.so")
 
 MSW_OK = 0
 MSW_E_INVALID = -1

@@ -20,10 +20,10 @@ constexpr int kMaxWinLen = 4096;
 constexpr int kLead = 32;              // sentinel words in front of each window stream
 
 // u32 words per lane-group stream: kLead + (max_win + 31) steps rounded to even
-// + 2 lookahead,
+// + 4 lookahead,
 // rounded so that the four groups of a wave start 16 banks apart (== 16 mod 32).
 inline uint32_t stream_stride(uint32_t max_win_len) {
-    uint32_t words = kLead + max_win_len + 2 * kGroupLanes + 3;
+    uint32_t words = kLead + max_win_len + 2 * kGroupLanes + 5;
     words = (words + 31u) & ~31u;
     return words + 16u;
 }
@@ -48,7 +48,8 @@ struct SwParams {
     uint32_t match2;          // match, duplicated into both u16 halves
     uint32_t delta2;          // match - mismatch
     uint32_t gap2;            // linear: gap penalty; affine: gap_extend
-    uint32_t open_ext2;       // affine: gap_open + gap_extend
+    uint32_t open_ext2;       // affine: gap_open + gap_extend + K
+    uint32_t bias2;           // affine: K = 64 + gap_extend (see msw_kernels.hip)
 };
 
 // Packed rows per lane for a read-length bound: ceil(m / 16) in the pairs

@@ -253,9 +253,10 @@ __device__ __forceinline__ void store_score(const SwParams& p, bool valid, uint3
     if (valid) p.score[pair] = (int32_t)s;
 }
 
-__device__ __forceinline__ void store_hit(const SwParams& p, bool valid, uint32_t pair, uint64_t key) {
+__device__ __forceinline__ void store_hit(const SwParams& p, bool valid, uint32_t pair, uint64_t key,
+                                          uint32_t bias) {
     if (!valid) return;
-    const uint32_t s = (uint32_t)(key >> 32);
+    const uint32_t s = (uint32_t)(key >> 32) - bias;
     p.score[pair] = (int32_t)s;
     if (p.end_i) {
         const uint32_t lo = (uint32_t)key;
@@ -267,7 +268,8 @@ __device__ __forceinline__ void store_hit(const SwParams& p, bool valid, uint32_
 // Per-row keys (h << 16 | 0xFFFF - j, one per u16 half) -> best hits.
 template <int KR, bool SPLIT>
 __device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta& q, int lg,
-                                              const uint32_t (&key_a)[KR], const uint32_t (&key_b)[KR]) {
+                                              const uint32_t (&key_a)[KR], const uint32_t (&key_b)[KR],
+                                              uint32_t bias) {
     uint64_t ga = 0, gb = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
@@ -283,26 +285,27 @@ __device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta&
     if constexpr (SPLIT) {
         ga = gb > ga ? gb : ga;
         ga = group_max_u64(ga);
-        if (lg == 0) store_hit(p, q.va, q.pa, ga);
+        if (lg == 0) store_hit(p, q.va, q.pa, ga, bias);
     } else {
         ga = group_max_u64(ga);
         gb = group_max_u64(gb);
         if (lg == 0) {
-            store_hit(p, q.va, q.pa, ga);
-            store_hit(p, q.vb, q.pb, gb);
+            store_hit(p, q.va, q.pa, ga, bias);
+            store_hit(p, q.vb, q.pb, gb, bias);
         }
     }
 }
 
 template <bool SPLIT>
-__device__ __forceinline__ void finish_score(const SwParams& p, const PairMeta& q, int lg, uint32_t best) {
+__device__ __forceinline__ void finish_score(const SwParams& p, const PairMeta& q, int lg, uint32_t best,
+                                             uint32_t bias) {
     best = group_pk_max(best);
     if (lg == 0) {
         if constexpr (SPLIT) {
-            store_score(p, q.va, q.pa, max(best & 0xFFFFu, best >> 16));
+            store_score(p, q.va, q.pa, max(best & 0xFFFFu, best >> 16) - bias);
         } else {
-            store_score(p, q.va, q.pa, best & 0xFFFFu);
-            store_score(p, q.vb, q.pb, best >> 16);
+            store_score(p, q.va, q.pa, (best & 0xFFFFu) - bias);
+            store_score(p, q.vb, q.pb, (best >> 16) - bias);
         }
     }
 }
@@ -322,12 +325,14 @@ __device__ __forceinline__ uint32_t from_above(uint32_t own_bottom) {
 //   linear:  a  = min(rc ^ w, delta)            substitution penalty 0 / delta
 //            t1 = sat(DG - a)                   DG = H_diag + match -> max(H_diag + s, 0)
 //            h  = max3(t1, E_left, E_up)        E = sat(H - gap)
-//   affine:  E  = max(sat(E_left - ge), G_left) G = sat(H - go - ge)
-//            F  = max(sat(F_up - ge),   G_up)
-//            h  = max3(t1, E, F)
-//   DG(next row, next column) = h + match.
-// All t1 of a step are formed first (they only read last step's values), so
-// h + match of row r can land in the register row r+1 just consumed.
+//   affine:  every H, E, F and t1 carries a bias K = 64 + ge (H* = H + K),
+//            which keeps all their subtractions non-negative per u16 half, so
+//            they run as full-rate v_sub_u32/v_add_u32 on the packed pair:
+//            t1* = (H*_diag + match) - a          (may sit below K: negative)
+//            E*  = max(E*_left - ge, GK_left)     GK = sat(H* - (go+ge+K)) + K
+//            F*  = max(F*_up   - ge, GK_up)       = max(H - go - ge, 0) + K
+//            h*  = max3(t1*, E*, F*)  >= K: the zero floor comes from GK.
+//   DG(next row, next column) = h + match, formed in the row chain (below).
 // ---------------------------------------------------------------------------
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
 __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint32_t* lds) {
@@ -344,15 +349,17 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
     __syncthreads();
 
     const uint32_t match2 = p.match2, delta2 = p.delta2, ext2 = p.gap2, oe2 = p.open_ext2;
-    uint32_t E[KR], G[AFFINE ? KR : 1];
+    const uint32_t bias2 = AFFINE ? p.bias2 : 0u;           // K in both halves (affine)
+    const uint32_t kmatch2 = add_nc(bias2, match2);
+    uint32_t E[KR], GK[AFFINE ? KR : 1];
     uint32_t key_a[COORDS ? KR : 1], key_b[COORDS ? KR : 1];
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
-        E[r] = 0u;
-        if constexpr (AFFINE) G[r] = 0u;
+        E[r] = bias2;                                        // E = 0 (affine: E* = K)
+        if constexpr (AFFINE) GK[r] = bias2;                 // G = 0
         if constexpr (COORDS) { key_a[r] = 0u; key_b[r] = 0u; }
     }
-    uint32_t f_bot = 0u, h_bot = 0u;
+    uint32_t f_bot = bias2, h_bot = bias2;                   // F = 0, H = 0
     uint32_t best = 0u;
     // lane reads column t - lg (pairs) / t - 2lg (split) at stream index kLead + that
     const uint32_t* wp = stream + (kLead - (SPLIT ? 2 * lg : lg));
@@ -366,22 +373,23 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
     {
         const uint32_t w0 = wp[0];
 #pragma unroll
-        for (int r = 0; r < KR; ++r) t1a[r] = pk_satsub(match2, pk_min(rc[r] ^ w0, delta2));
+        for (int r = 0; r < KR; ++r) {
+            const uint32_t a = pk_min(rc[r] ^ w0, delta2);
+            t1a[r] = AFFINE ? kmatch2 - a : pk_satsub(match2, a);
+        }
     }
-    uint32_t w_next = wp[1];  // one step of LDS lookahead
-
     // One wavefront step: consumes t1 (this step's diagonal terms), produces
-    // t1n (the next step's).  Called with alternating buffers so the hand-over
-    // needs no register copies.
-    auto step = [&](int t, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR]) __attribute__((always_inline)) {
-        const uint32_t w = w_next;  // window codes of step t + 1
-        w_next = wp[t + 2];
-        const uint32_t d_up = add_nc(from_above<SPLIT>(h_bot), match2);
-        uint32_t up;    // linear: E of the row above; affine: F of the row above
-        uint32_t g_up;  // affine: G of the row above
+    // t1n (the next step's) from w, the window codes of step t + 1.  Called
+    // with alternating buffers so the hand-over needs no register copies.
+    auto step = [&](int t, uint32_t w, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR]) __attribute__((always_inline)) {
+        // Unbiased values cross the lanes (the zero fill is the top boundary),
+        // the bias is re-added on arrival: no u16 half ever goes negative.
+        const uint32_t d_up = add_nc(from_above<SPLIT>(h_bot - bias2), kmatch2);
+        uint32_t up;    // linear: E of the row above; affine: F* of the row above
+        uint32_t g_up;  // affine: GK of the row above
         if constexpr (AFFINE) {
-            up = from_above<SPLIT>(f_bot);
-            g_up = from_above<SPLIT>(G[KR - 1]);
+            up = add_nc(from_above<SPLIT>(f_bot - bias2), bias2);
+            g_up = add_nc(from_above<SPLIT>(GK[KR - 1] - bias2), bias2);
         } else {
             up = from_above<SPLIT>(E[KR - 1]);
             g_up = 0u;
@@ -389,7 +397,8 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
         uint32_t a_n[KR];
 #pragma unroll
         for (int r = 0; r < KR; ++r) a_n[r] = pk_min(rc[r] ^ w, delta2);
-        t1n[0] = pk_satsub(d_up, a_n[0]);  // row 0's diagonal next step: the lane above's H now
+        // row 0's diagonal next step: the lane above's H now
+        t1n[0] = AFFINE ? d_up - a_n[0] : pk_satsub(d_up, a_n[0]);
         const uint32_t nj_a = (nj_lane - (uint32_t)t) & 0xFFFFu;
         const uint32_t nj_b = SPLIT ? ((nj_lane + 1u - (uint32_t)t) & 0xFFFFu) : nj_a;
         uint32_t hprev = 0u;
@@ -397,17 +406,18 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
         for (int r = 0; r < KR; ++r) {
             uint32_t h;
             if constexpr (AFFINE) {
-                const uint32_t e = pk_max(pk_satsub(E[r], ext2), G[r]);
-                up = pk_max(pk_satsub(up, ext2), g_up);
+                const uint32_t e = pk_max(E[r] - ext2, GK[r]);     // full-rate sub, no borrow
+                up = pk_max(up - ext2, g_up);
                 h = pk_max3(t1[r], e, up);
                 E[r] = e;
-                g_up = G[r] = pk_satsub(h, oe2);
+                g_up = GK[r] = add_nc(pk_satsub(h, oe2), bias2);   // oe2 = go + ge + K
+                if (r + 1 < KR) t1n[r + 1] = add_nc(h, match2) - a_n[r + 1];
             } else {
                 h = pk_max3(t1[r], E[r], up);
                 up = E[r] = pk_satsub(h, ext2);
+                if (r + 1 < KR) t1n[r + 1] = pk_satsub(add_nc(h, match2), a_n[r + 1]);
             }
-            if (r + 1 < KR) t1n[r + 1] = pk_satsub(add_nc(h, match2), a_n[r + 1]);
-            else h_bot = h;
+            if (r + 1 == KR) h_bot = h;
             if constexpr (COORDS) {
                 key_a[r] = max(key_a[r], (h << 16) | nj_a);
                 key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj_b);
@@ -421,13 +431,26 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
     };
     // Step count rounded up to even: the extra step scores sentinel columns,
     // which never reach a real cell's score.
+    // The window codes are read from LDS one full iteration (two steps) before
+    // use, so a lone wave never waits on LDS latency.  The read is an asm
+    // statement (hipcc would otherwise sink it to the consuming iteration); its
+    // wait names the destination, so nothing reads it before the data lands.
+    uint32_t w1 = wp[1], w2 = wp[2];
+    const uint32_t lds_wp = (uint32_t)(uintptr_t)wp;  // LDS byte address of wp[0]
+    uint2 wn;
+    asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wn) : "v"(lds_wp));
     for (int t = 0; t < steps; t += 2) {
-        step(t, t1a, t1b);
-        step(t + 1, t1b, t1a);
+        step(t, w1, t1a, t1b);
+        step(t + 1, w2, t1b, t1a);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
+        w1 = wn.x;
+        w2 = wn.y;
+        asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wn) : "v"(lds_wp + 4u * (uint32_t)(t + 2)));
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
 
-    if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, key_a, key_b);
-    else finish_score<SPLIT>(p, q, lg, best);
+    if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, key_a, key_b, bias2 & 0xFFFFu);
+    else finish_score<SPLIT>(p, q, lg, best, bias2 & 0xFFFFu);
 }
 
 // One layout for the whole grid.

@@ -68,8 +68,9 @@ inline uint32_t dup16(uint32_t v) { return (v & 0xFFFFu) | ((v & 0xFFFFu) << 16)
 // Validated kernel constants for one scoring scheme.
 struct Scheme {
     bool affine, coords;
-    uint32_t match2, delta2, gap2, open_ext2, code_shift;
+    uint32_t match2, delta2, gap2, open_ext2, bias2, code_shift;
     int32_t match;
+    uint32_t bias;  // affine value bias K (0 for linear)
 };
 
 int make_scheme(const msw_scoring_t* sc, Scheme* s) {
@@ -81,8 +82,8 @@ int make_scheme(const msw_scoring_t* sc, Scheme* s) {
     if (sc->gap_extend < 0 || sc->gap_open < 0)
         return fail(MSW_E_RANGE, "negative gap penalty (open=%d extend=%d)", sc->gap_open,
                     sc->gap_extend);
-    if (sc->gap_extend > 30000 || sc->gap_open > 30000)
-        return fail(MSW_E_RANGE, "gap penalty too large");
+    if (sc->gap_extend > 1024 || sc->gap_open > 30000)
+        return fail(MSW_E_RANGE, "gap penalty too large (gap_extend <= 1024, gap_open <= 30000)");
     s->affine = sc->affine != 0;
     s->coords = sc->want_coords != 0;
     s->match = sc->match;
@@ -93,7 +94,10 @@ int make_scheme(const msw_scoring_t* sc, Scheme* s) {
     s->match2 = dup16((uint32_t)sc->match);
     s->delta2 = dup16(delta);
     s->gap2 = dup16((uint32_t)sc->gap_extend);
-    s->open_ext2 = dup16((uint32_t)(sc->gap_open + sc->gap_extend));
+    // Affine kernels keep H/E/F biased by K = 64 + gap_extend (msw_kernels.hip).
+    s->bias = s->affine ? 64u + (uint32_t)sc->gap_extend : 0u;
+    s->bias2 = dup16(s->bias);
+    s->open_ext2 = dup16((uint32_t)(sc->gap_open + sc->gap_extend) + s->bias);
     return MSW_OK;
 }
 
@@ -104,7 +108,7 @@ int check_bounds(const Scheme& s, uint32_t max_m, uint32_t max_n) {
         return fail(MSW_E_RANGE, "read length %u > %d", max_m, msw::kMaxReadLen);
     if (max_n > (uint32_t)msw::kMaxWinLen)
         return fail(MSW_E_RANGE, "window length %u > %d", max_n, msw::kMaxWinLen);
-    const uint64_t bound = (uint64_t)s.match * (std::min(max_m, max_n) + 1u);
+    const uint64_t bound = (uint64_t)s.match * (std::min(max_m, max_n) + 2u) + s.bias;
     if (bound >= 0x7C00u)
         return fail(MSW_E_RANGE, "match*(len+1)=%llu exceeds the 16-bit score range",
                     (unsigned long long)bound);
@@ -119,6 +123,7 @@ msw::SwParams base_params(const Scheme& s) {
     p.delta2 = s.delta2;
     p.gap2 = s.gap2;
     p.open_ext2 = s.open_ext2;
+    p.bias2 = s.bias2;
     return p;
 }
 
