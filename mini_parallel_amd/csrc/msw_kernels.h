@@ -49,7 +49,8 @@ struct SwParams {
     uint32_t delta2;          // match - mismatch
     uint32_t gap2;            // linear: gap penalty; affine: gap_extend
     uint32_t open_ext2;       // affine: gap_open + gap_extend + K
-    uint32_t bias2;           // affine: K = 64 + gap_extend (see msw_kernels.hip)
+    uint32_t bias2;           // affine: K = 256 + gap_extend (see msw_kernels.hip)
+    uint64_t* trace;          // diagnostics (MSW_WAVE_TRACE): 4 words per block, or nullptr
 };
 
 // Packed rows per lane for a read-length bound: ceil(m / 16) in the pairs

@@ -26,6 +26,8 @@
 //    per-cell masking is needed: such cells never reach the pair's score.
 #include "msw_kernels.h"
 
+#include <type_traits>
+
 namespace msw {
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -321,11 +323,63 @@ __device__ __forceinline__ uint32_t from_above(uint32_t own_bottom) {
 }
 
 // ---------------------------------------------------------------------------
+// ACGT fast path.  When every window byte of a wave is one of A, C, G, T, the
+// substitution penalty of a packed cell pair is one v_perm_b32 lookup
+// instead of v_xor + v_pk_min: each packed row keeps two 4-byte tables
+// (lo half in bytes 0-3, hi half in bytes 4-7: byte k = 0 if the row's base has
+// class k, else delta), and each window column's LDS word becomes a selector
+// {class(lo), 12, 4 + class(hi), 12} (selector 12 reads 0x00, 13 reads 0xFF:
+// padding columns score a = 0xFF, below every real cell as with the sentinel
+// codes).  The class of A/C/G/T is ((b >> 1) ^ (b >> 2)) & 3 = 0/1/2/3.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t base_class(uint32_t b) { return ((b >> 1) ^ (b >> 2)) & 3u; }
+
+__device__ __forceinline__ bool is_acgt(uint32_t b) {
+    const uint32_t o = b - 0x41u;  // A C G T = 0x41 + {0, 2, 6, 19}
+    return o < 20u && ((0x80045u >> o) & 1u);
+}
+
+// u16 window code half (byte << shift or the sentinel) -> fast path possible
+__device__ __forceinline__ bool code_ok(uint32_t v, uint32_t shift) {
+    return (v & kWinSentinel) || is_acgt(v >> shift);
+}
+
+__device__ __forceinline__ uint32_t win_selector(uint32_t word, uint32_t shift) {
+    const uint32_t lo = word & 0xFFFFu, hi = word >> 16;
+    const uint32_t sl = (lo & kWinSentinel) ? 13u : base_class(lo >> shift);
+    const uint32_t sh = (hi & kWinSentinel) ? 13u : base_class(hi >> shift);
+    return sl | (12u << 8) | ((4u + sh) << 16) | (12u << 24);
+}
+
+// A read byte outside A/C/G/T (N, lower case, ...) can never equal a window
+// byte of a fast-path wave, so its row (like a padding row) is all delta.
+__device__ __forceinline__ uint32_t row_table(uint32_t v, uint32_t shift, uint32_t d4) {
+    const uint32_t b = v >> shift;
+    return ((v & kReadSentinel) || !is_acgt(b)) ? d4 : d4 & ~(0xFFu << (8u * base_class(b)));
+}
+
+// Checks this lane's share of the group's staged window stream; returns true
+// (wave-uniform) if every window byte of the wave is A/C/G/T, and then
+// rewrites the stream in place as selectors.  Reads may hold any byte.
+__device__ __forceinline__ bool to_fast_path(uint32_t* stream, int words, int lg, uint32_t shift) {
+    bool ok = true;
+    for (int k = lg; k < words; k += kGroupLanes) {
+        const uint32_t w = stream[k];
+        ok = ok && code_ok(w & 0xFFFFu, shift) && code_ok(w >> 16, shift);
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
+    for (int k = lg; k < words; k += kGroupLanes) stream[k] = win_selector(stream[k], shift);
+    __syncthreads();
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // The DP.  Per packed cell pair (same (i, j) in both halves):
 //   linear:  a  = min(rc ^ w, delta)            substitution penalty 0 / delta
 //            t1 = sat(DG - a)                   DG = H_diag + match -> max(H_diag + s, 0)
 //            h  = max3(t1, E_left, E_up)        E = sat(H - gap)
-//   affine:  every H, E, F and t1 carries a bias K = 64 + ge (H* = H + K),
+//   (fast path: a = perm(table_hi, table_lo, selector), see above)
+//   affine:  every H, E, F and t1 carries a bias K = 256 + ge (H* = H + K),
 //            which keeps all their subtractions non-negative per u16 half, so
 //            they run as full-rate v_sub_u32/v_add_u32 on the packed pair:
 //            t1* = (H*_diag + match) - a          (may sit below K: negative)
@@ -335,7 +389,7 @@ __device__ __forceinline__ uint32_t from_above(uint32_t own_bottom) {
 //   DG(next row, next column) = h + match, formed in the row chain (below).
 // ---------------------------------------------------------------------------
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
-__device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint32_t* lds) {
+__device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint32_t* lds) {
     const int lane = threadIdx.x;
     const int g = lane >> 4, lg = lane & 15;
     const PairMeta q = load_meta<SPLIT>(p, g, block);
@@ -351,113 +405,177 @@ __device__ __forceinline__ void sw_body(const SwParams& p, uint32_t block, uint3
     const uint32_t match2 = p.match2, delta2 = p.delta2, ext2 = p.gap2, oe2 = p.open_ext2;
     const uint32_t bias2 = AFFINE ? p.bias2 : 0u;           // K in both halves (affine)
     const uint32_t kmatch2 = add_nc(bias2, match2);
+    const uint32_t og2 = oe2 - bias2;                       // affine: go + ge
     uint32_t E[KR], GK[AFFINE ? KR : 1];
     uint32_t key_a[COORDS ? KR : 1], key_b[COORDS ? KR : 1];
-#pragma unroll
-    for (int r = 0; r < KR; ++r) {
-        E[r] = bias2;                                        // E = 0 (affine: E* = K)
-        if constexpr (AFFINE) GK[r] = bias2;                 // G = 0
-        if constexpr (COORDS) { key_a[r] = 0u; key_b[r] = 0u; }
-    }
-    uint32_t f_bot = bias2, h_bot = bias2;                   // F = 0, H = 0
     uint32_t best = 0u;
     // lane reads column t - lg (pairs) / t - 2lg (split) at stream index kLead + that
     const uint32_t* wp = stream + (kLead - (SPLIT ? 2 * lg : lg));
     const uint32_t nj_lane = (uint32_t)(0xFFFF + (SPLIT ? 2 * lg : lg));
-
-    // Software pipeline: t1 (the diagonal term) of step t+1 is formed inside
-    // step t's row chain, as soon as the H it needs is known, so each link of
-    // the dependent max3 -> sat-sub chain has independent work beside it
-    // (waves issue in order; a lone wave otherwise stalls on every link).
-    uint32_t t1a[KR], t1b[KR];
-    {
-        const uint32_t w0 = wp[0];
-#pragma unroll
-        for (int r = 0; r < KR; ++r) {
-            const uint32_t a = pk_min(rc[r] ^ w0, delta2);
-            t1a[r] = AFFINE ? kmatch2 - a : pk_satsub(match2, a);
-        }
-    }
-    // One wavefront step: consumes t1 (this step's diagonal terms), produces
-    // t1n (the next step's) from w, the window codes of step t + 1.  Called
-    // with alternating buffers so the hand-over needs no register copies.
-    auto step = [&](int t, uint32_t w, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR]) __attribute__((always_inline)) {
-        // Unbiased values cross the lanes (the zero fill is the top boundary),
-        // the bias is re-added on arrival: no u16 half ever goes negative.
-        const uint32_t d_up = add_nc(from_above<SPLIT>(h_bot - bias2), kmatch2);
-        uint32_t up;    // linear: E of the row above; affine: F* of the row above
-        uint32_t g_up;  // affine: GK of the row above
-        if constexpr (AFFINE) {
-            up = add_nc(from_above<SPLIT>(f_bot - bias2), bias2);
-            g_up = add_nc(from_above<SPLIT>(GK[KR - 1] - bias2), bias2);
-        } else {
-            up = from_above<SPLIT>(E[KR - 1]);
-            g_up = 0u;
-        }
-        uint32_t a_n[KR];
-#pragma unroll
-        for (int r = 0; r < KR; ++r) a_n[r] = pk_min(rc[r] ^ w, delta2);
-        // row 0's diagonal next step: the lane above's H now
-        t1n[0] = AFFINE ? d_up - a_n[0] : pk_satsub(d_up, a_n[0]);
-        const uint32_t nj_a = (nj_lane - (uint32_t)t) & 0xFFFFu;
-        const uint32_t nj_b = SPLIT ? ((nj_lane + 1u - (uint32_t)t) & 0xFFFFu) : nj_a;
-        uint32_t hprev = 0u;
-#pragma unroll
-        for (int r = 0; r < KR; ++r) {
-            uint32_t h;
-            if constexpr (AFFINE) {
-                const uint32_t e = pk_max(E[r] - ext2, GK[r]);     // full-rate sub, no borrow
-                up = pk_max(up - ext2, g_up);
-                h = pk_max3(t1[r], e, up);
-                E[r] = e;
-                g_up = GK[r] = add_nc(pk_satsub(h, oe2), bias2);   // oe2 = go + ge + K
-                if (r + 1 < KR) t1n[r + 1] = add_nc(h, match2) - a_n[r + 1];
-            } else {
-                h = pk_max3(t1[r], E[r], up);
-                up = E[r] = pk_satsub(h, ext2);
-                if (r + 1 < KR) t1n[r + 1] = pk_satsub(add_nc(h, match2), a_n[r + 1]);
-            }
-            if (r + 1 == KR) h_bot = h;
-            if constexpr (COORDS) {
-                key_a[r] = max(key_a[r], (h << 16) | nj_a);
-                key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj_b);
-            } else {
-                if (r & 1) best = track_max3(best, hprev, h);
-                else if (r + 1 == KR) best = pk_max(best, h);
-                hprev = h;
-            }
-        }
-        if constexpr (AFFINE) f_bot = up;
-    };
-    // Step count rounded up to even: the extra step scores sentinel columns,
-    // which never reach a real cell's score.
-    // The window codes are read from LDS one full iteration (two steps) before
-    // use, so a lone wave never waits on LDS latency.  The read is an asm
-    // statement (hipcc would otherwise sink it to the consuming iteration); its
-    // wait names the destination, so nothing reads it before the data lands.
-    uint32_t w1 = wp[1], w2 = wp[2];
     const uint32_t lds_wp = (uint32_t)(uintptr_t)wp;  // LDS byte address of wp[0]
-    uint2 wn;
-    asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wn) : "v"(lds_wp));
-    for (int t = 0; t < steps; t += 2) {
-        step(t, w1, t1a, t1b);
-        step(t + 1, w2, t1b, t1a);
+
+    // The whole DP for one substitution scheme: PERM = ACGT table lookups,
+    // else xor/min on the byte codes.
+    auto run = [&](auto perm_tag) __attribute__((always_inline)) {
+        constexpr bool PERM = decltype(perm_tag)::value;
+        uint32_t tab_lo[PERM ? KR : 1], tab_hi[PERM ? KR : 1];
+        if constexpr (PERM) {
+            const uint32_t d4 = (delta2 & 0xFFu) * 0x01010101u;
+#pragma unroll
+            for (int r = 0; r < KR; ++r) {
+                tab_lo[r] = row_table(rc[r] & 0xFFFFu, p.code_shift, d4);
+                tab_hi[r] = row_table(rc[r] >> 16, p.code_shift, d4);
+            }
+        }
+        auto sub = [&](int r, uint32_t w) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (PERM) return __builtin_amdgcn_perm(tab_hi[r], tab_lo[r], w);
+            else return pk_min(rc[r] ^ w, delta2);
+        };
+#pragma unroll
+        for (int r = 0; r < KR; ++r) {
+            E[r] = bias2;                                    // E = 0 (affine: E* = K)
+            if constexpr (AFFINE) GK[r] = bias2;             // G = 0
+            if constexpr (COORDS) { key_a[r] = 0u; key_b[r] = 0u; }
+        }
+        uint32_t f_bot = bias2, h_bot = bias2;               // F = 0, H = 0
+
+        // Software pipeline: t1 (the diagonal term) of step t+1 is formed inside
+        // step t's row chain, as soon as the H it needs is known, so each link of
+        // the dependent max3 -> sat-sub chain has independent work beside it
+        // (waves issue in order; a lone wave otherwise stalls on every link).
+        uint32_t t1a[KR], t1b[KR];
+        {
+            const uint32_t w0 = wp[0];
+#pragma unroll
+            for (int r = 0; r < KR; ++r) {
+                const uint32_t a = sub(r, w0);
+                t1a[r] = AFFINE ? kmatch2 - a : pk_satsub(match2, a);
+            }
+        }
+        // One wavefront step: consumes t1 (this step's diagonal terms), produces
+        // t1n (the next step's) from w, the window word of step t + 1.  Called
+        // with alternating buffers so the hand-over needs no register copies.
+        auto step = [&](int t, uint32_t w, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR])
+                        __attribute__((always_inline)) {
+            // Unbiased values cross the lanes (the zero fill is the top boundary),
+            // the bias is re-added on arrival: no u16 half ever goes negative.
+            // Only H (and affine F) cross: E resp. GK of the row above are
+            // functions of its H, recomputed here instead of a second DPP move.
+            const uint32_t h_up = from_above<SPLIT>(h_bot - bias2);
+            const uint32_t d_up = add_nc(h_up, kmatch2);
+            uint32_t up;    // linear: E of the row above; affine: F* of the row above
+            uint32_t g_up;  // affine: GK of the row above
+            if constexpr (AFFINE) {
+                up = add_nc(from_above<SPLIT>(f_bot - bias2), bias2);
+                g_up = add_nc(pk_satsub(h_up, og2), bias2);
+            } else {
+                up = pk_satsub(h_up, ext2);
+                g_up = 0u;
+            }
+            uint32_t a_n[KR];
+#pragma unroll
+            for (int r = 0; r < KR; ++r) a_n[r] = sub(r, w);
+            // row 0's diagonal next step: the lane above's H now
+            t1n[0] = AFFINE ? d_up - a_n[0] : pk_satsub(d_up, a_n[0]);
+            const uint32_t nj_a = (nj_lane - (uint32_t)t) & 0xFFFFu;
+            const uint32_t nj_b = SPLIT ? ((nj_lane + 1u - (uint32_t)t) & 0xFFFFu) : nj_a;
+            uint32_t hprev = 0u;
+#pragma unroll
+            for (int r = 0; r < KR; ++r) {
+                uint32_t h;
+                if constexpr (AFFINE) {
+                    const uint32_t e = pk_max(E[r] - ext2, GK[r]);     // full-rate sub, no borrow
+                    up = pk_max(up - ext2, g_up);
+                    h = pk_max3(t1[r], e, up);
+                    E[r] = e;
+                    g_up = GK[r] = add_nc(pk_satsub(h, oe2), bias2);   // oe2 = go + ge + K
+                    if (r + 1 < KR) t1n[r + 1] = add_nc(h, match2) - a_n[r + 1];
+                } else {
+                    h = pk_max3(t1[r], E[r], up);
+                    up = E[r] = pk_satsub(h, ext2);
+                    if (r + 1 < KR) t1n[r + 1] = pk_satsub(add_nc(h, match2), a_n[r + 1]);
+                }
+                if (r + 1 == KR) h_bot = h;
+                if constexpr (COORDS) {
+                    key_a[r] = max(key_a[r], (h << 16) | nj_a);
+                    key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj_b);
+                } else {
+                    if (r & 1) best = track_max3(best, hprev, h);
+                    else if (r + 1 == KR) best = pk_max(best, h);
+                    hprev = h;
+                }
+            }
+            if constexpr (AFFINE) f_bot = up;
+        };
+        // Step count rounded up to even: the extra step scores sentinel columns,
+        // which never reach a real cell's score.
+        // The window words are read from LDS one full iteration (two steps) before
+        // use, so a lone wave never waits on LDS latency.  The read is an asm
+        // statement (hipcc would otherwise sink it to the consuming iteration); its
+        // wait names the destination, so nothing reads it before the data lands.
+        uint32_t w1 = wp[1], w2 = wp[2];
+        uint2 wn;
+        asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wn) : "v"(lds_wp));
+        for (int t = 0; t < steps; t += 2) {
+            step(t, w1, t1a, t1b);
+            step(t + 1, w2, t1b, t1a);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
+            w1 = wn.x;
+            w2 = wn.y;
+            asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4"
+                         : "=v"(wn) : "v"(lds_wp + 4u * (uint32_t)(t + 2)));
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
-        w1 = wn.x;
-        w2 = wn.y;
-        asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wn) : "v"(lds_wp + 4u * (uint32_t)(t + 2)));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
+    };
+    // Words of the group's stream the loop consumes (all staged).
+    const int words = kLead + steps;
+    const bool fast = to_fast_path(stream, words, lg, p.code_shift);
+    if (fast) run(std::true_type{});
+    else run(std::false_type{});
 
     if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, key_a, key_b, bias2 & 0xFFFFu);
     else finish_score<SPLIT>(p, q, lg, best, bias2 & 0xFFFFu);
+    return fast;
+}
+
+// Diagnostics (MSW_WAVE_TRACE, tools/wave_trace.py): per block, start and end
+// on the 100 MHz constant clock, the shader-clock cycles between them, the
+// wave's HW_ID / XCC_ID and what it ran.
+struct WaveClock {
+    uint64_t t0, c0;
+};
+__device__ __forceinline__ WaveClock trace_begin(const SwParams& p) {
+    WaveClock w{0, 0};
+    if (p.trace) {
+        w.t0 = __builtin_amdgcn_s_memrealtime();
+        w.c0 = __builtin_amdgcn_s_memtime();
+    }
+    return w;
+}
+__device__ __forceinline__ void trace_end(const SwParams& p, const WaveClock& w, bool fast, bool split,
+                                          int kr) {
+    if (!p.trace) return;
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {
+        const uint32_t hw_id = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11));    // HW_REG_XCC_ID
+        uint64_t* o = p.trace + 4ull * blockIdx.x;
+        o[0] = w.t0;
+        o[1] = t1;
+        o[2] = (uint64_t)hw_id | ((uint64_t)xcc << 32) | ((uint64_t)fast << 40) | ((uint64_t)split << 41) |
+               ((uint64_t)kr << 48);
+        o[3] = c1 - w.c0;
+    }
 }
 
 // One layout for the whole grid.
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
 __global__ __launch_bounds__(64) void sw_kernel(SwParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    sw_body<KR, AFFINE, COORDS, SPLIT>(p, blockIdx.x, lds);
+    const WaveClock wc = trace_begin(p);
+    const bool fast = sw_body<KR, AFFINE, COORDS, SPLIT>(p, blockIdx.x, lds);
+    trace_end(p, wc, fast, SPLIT, KR);
 }
 
 // Mixed grid for small batches: blocks [0, p.pairs_blocks) run the pairs
@@ -468,15 +586,18 @@ __global__ __launch_bounds__(64) void sw_kernel(SwParams p) {
 template <int KRP, bool AFFINE, bool COORDS>
 __global__ __launch_bounds__(64) void sw_mixed_kernel(SwParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const WaveClock wc = trace_begin(p);
     if (blockIdx.x < p.pairs_blocks) {
-        sw_body<KRP, AFFINE, COORDS, false>(p, blockIdx.x, lds);
+        const bool fast = sw_body<KRP, AFFINE, COORDS, false>(p, blockIdx.x, lds);
+        trace_end(p, wc, fast, false, KRP);
     } else {
         SwParams q = p;
         const uint32_t done = p.pairs_blocks * (uint32_t)kPairsPerWave;
         q.n_slots = p.n_slots - done;
         q.order = p.order ? p.order + done : nullptr;
         if (!p.order) q.slot_base = done;
-        sw_body<(KRP + 1) / 2, AFFINE, COORDS, true>(q, blockIdx.x - p.pairs_blocks, lds);
+        const bool fast = sw_body<(KRP + 1) / 2, AFFINE, COORDS, true>(q, blockIdx.x - p.pairs_blocks, lds);
+        trace_end(p, wc, fast, true, (KRP + 1) / 2);
     }
 }
 

@@ -94,8 +94,9 @@ int make_scheme(const msw_scoring_t* sc, Scheme* s) {
     s->match2 = dup16((uint32_t)sc->match);
     s->delta2 = dup16(delta);
     s->gap2 = dup16((uint32_t)sc->gap_extend);
-    // Affine kernels keep H/E/F biased by K = 64 + gap_extend (msw_kernels.hip).
-    s->bias = s->affine ? 64u + (uint32_t)sc->gap_extend : 0u;
+    // Affine kernels keep H/E/F biased by K = 256 + gap_extend (msw_kernels.hip):
+    // K > 0xFF, the largest substitution penalty (fast-path padding columns).
+    s->bias = s->affine ? 256u + (uint32_t)sc->gap_extend : 0u;
     s->bias2 = dup16(s->bias);
     s->open_ext2 = dup16((uint32_t)(sc->gap_open + sc->gap_extend) + s->bias);
     return MSW_OK;
@@ -560,6 +561,31 @@ int msw_wait(msw_ctx* ctx, uint64_t ticket) {
     return MSW_OK;
 }
 
+// Diagnostics only (MSW_WAVE_TRACE=file, read by tools/wave_trace.py): the
+// launch records per-block clocks and placement and appends one record
+// {u64 n_blocks, u64 layout, n_blocks x 4 u64} to the file.  Synchronous.
+static int traced_launch(msw::SwParams p, const Scheme& sch, uint32_t max_read_len, const LaunchPlan& plan,
+                         hipStream_t st, const char* path) {
+    const uint64_t n_blocks = p.n_slots / 4 + 2;  // the split layout's count bounds every grid
+    uint64_t* d = nullptr;
+    HIP_TRY(hipMalloc(&d, n_blocks * 4 * sizeof(uint64_t)));
+    (void)hipMemsetAsync(d, 0, n_blocks * 4 * sizeof(uint64_t), st);
+    p.trace = d;
+    hipError_t e = msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    std::vector<uint64_t> h(n_blocks * 4);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), d, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(MSW_E_DEVICE, "traced launch: %s", hipGetErrorString(e));
+    FILE* f = fopen(path, "ab");
+    if (!f) return fail(MSW_E_INVALID, "cannot open MSW_WAVE_TRACE file %s", path);
+    const uint64_t hdr[2] = {n_blocks, (uint64_t)plan.layout | ((uint64_t)plan.pairs_blocks << 8)};
+    fwrite(hdr, sizeof(hdr), 1, f);
+    fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+    fclose(f);
+    return MSW_OK;
+}
+
 int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* b, msw_out_t* out,
                            uint32_t max_read_len, uint32_t max_win_len, void* stream) {
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
@@ -589,6 +615,8 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
     const LaunchPlan plan = choose_layout(b->n_pairs, max_read_len, max_win_len, sch, ctx->cu_count);
     p.pairs_blocks = plan.pairs_blocks;
+    const char* trace_path = getenv("MSW_WAVE_TRACE");
+    if (trace_path && *trace_path) return traced_launch(p, sch, max_read_len, plan, st, trace_path);
     HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st));
     return MSW_OK;
 }

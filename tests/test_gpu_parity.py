@@ -142,6 +142,34 @@ def test_identical_and_all_mismatch(gpu_ctx, layout, oracle):
     assert all(got[0][72:] == 300)
 
 
+def test_acgt_fast_path_and_fallback(gpu_ctx, layout, oracle):
+    """Waves whose windows are pure A/C/G/T take the v_perm table path (reads
+    may hold any byte: N, lower case, bytes whose class formula collides with
+    A/C/G/T such as 'E', high-bit bytes); a window with any other byte sends its
+    wave down the xor/min path.  Both must agree with the oracle."""
+    rng = np.random.default_rng(31)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    zoo = np.frombuffer(b"ACGTACGTACGTNacgtEBDHS\x00\xc1\xc3\x41", np.uint8)
+    reads, wins = [], []
+    for k in range(1024):
+        m = int(rng.integers(1, 257))
+        n = int(rng.integers(1, 520))
+        r = bytes(rng.choice(zoo if k % 3 else acgt, m))
+        w = bytearray(rng.choice(acgt, n))
+        if k % 5 == 0:
+            w[int(rng.integers(0, n))] = int(rng.choice(np.frombuffer(b"NaEx\x00", np.uint8)))
+        if k % 7 == 0 and n > m:  # plant the read so long alignments exist
+            w[: m] = r
+        reads.append(r)
+        wins.append(bytes(w))
+    R, rl, W, wl = mpa.pack_batch(reads, wins)
+    b = B(R, rl, W, wl)
+    for sc in (Scoring(want_coords=True), Scoring(),
+               Scoring(gap_open=2, gap_extend=1, affine=True, want_coords=True),
+               Scoring(match=3, mismatch=-61, gap_open=7, gap_extend=1024, affine=True)):
+        assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), sc.want_coords)
+
+
 def test_async_and_chunking_agree(gpu_ctx, oracle):
     b = config_batch(2, n_pairs=5000, seed_offset=40)
     sc = Scoring(want_coords=True)
