@@ -34,11 +34,12 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 # VALU issue cycles per packed row-step (one wave instruction stream covering
-# 64 lanes x 2 cells = 128 cells), from the instruction mix of each kernel
-# variant and the per-op issue costs measured by tools/ubench_valu.hip
-# (half-rate packed/max ops 4.1 cycles, full-rate xor/add 2.2).
-CYCLES_PER_ROW_STEP = {"linear": 22.85, "linear_coords": 37.2, "affine": 43.35,
-                       "affine_coords": 53.6}
+# 64 lanes x 2 cells = 128 cells): the compiled loop's instruction mix (ACGT
+# fast path, KR = 10, tools/issue_sim.py cost table) priced at the per-op issue
+# costs measured by tools/ubench_valu.hip (packed/max/perm ops 4.1 cycles,
+# add 2.2, DPP 4.4).  The xor/min path costs +2.2.
+CYCLES_PER_ROW_STEP = {"linear": 21.82, "linear_coords": 32.51, "affine": 35.82,
+                       "affine_coords": 46.51}
 
 
 def parse():
@@ -55,7 +56,7 @@ def parse():
     return ap.parse_args()
 
 
-def load_pmc_traffic(kernel_prefix: str):
+def load_pmc_traffic(key: str):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -63,7 +64,7 @@ def load_pmc_traffic(kernel_prefix: str):
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel_prefix)
+        return d.get(key)
     except Exception:
         return None
 
@@ -158,7 +159,8 @@ def main():
         achieved = alg_bytes / avg_launch_s / 1e9
         kernel_gcups = cells / avg_launch_s / 1e9
         valu_ceiling = 128.0 / CYCLES_PER_ROW_STEP[kind] * SIMDS * CLOCK_HZ / 1e9
-        traffic = load_pmc_traffic(f"sw_{'affine' if scoring.affine else 'linear'}_kernel")
+        # PMC bytes exist only for the workload tools/profile_round.sh profiled
+        traffic = load_pmc_traffic(f"config{cfg}:{kind}") if not args.pairs else None
 
         cpu = None
         parity = None
@@ -219,7 +221,7 @@ def main():
                      "frac": round(kernel_gcups / valu_ceiling, 4),
                      "cycles_per_packed_row_step": CYCLES_PER_ROW_STEP[kind],
                      "basis": "VALU issue bound of the kernel's instruction mix at 2.4 GHz "
-                              "(DESIGN.md 4.3)"},
+                              "(peak clock; ~2.2 GHz sustained, tools/wave_trace.py; DESIGN.md 4)"},
             "cpu_baseline": cpu,
             "parity": parity,
             "gathered_scores": gathered,

@@ -50,7 +50,8 @@ def main():
             }
             kind = "sw_kernel" if "sw_kernel" in k else ("sw_mixed_kernel" if "mixed" in k else k)
             traffic[k] = traffic_entry
-            traffic.setdefault("sw_linear_kernel", traffic_entry)
+            # tools/profile_round.sh profiles the default bench workload
+            traffic.setdefault("config2:linear", traffic_entry)
         if "GRBM_GUI_ACTIVE" in d:
             summary[k]["note_clock"] = "effective clock = GRBM_GUI_ACTIVE / 8 / kernel time"
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
