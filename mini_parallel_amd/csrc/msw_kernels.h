@@ -51,23 +51,30 @@ struct SwParams {
     uint32_t open_ext2;       // affine: gap_open + gap_extend + K
     uint32_t bias2;           // affine: K = 256 + gap_extend (see msw_kernels.hip)
     uint64_t* trace;          // diagnostics (MSW_WAVE_TRACE): 4 words per block, or nullptr
+    uint32_t group_lanes;     // G: lanes per lane group (8..16)
+    uint32_t groups;          // lane groups per wave = 64 / G (lanes past groups * G idle)
 };
 
 // Packed rows per lane for a read-length bound: ceil(m / 16) in the pairs
 // layout, ceil(m / 32) in the split layout (each packed row holds two rows).
-inline int rows_per_lane(uint32_t max_read_len, bool split) {
-    const uint32_t per = split ? 2 * kGroupLanes : kGroupLanes;
+inline int rows_per_lane(uint32_t max_read_len, bool split, uint32_t group_lanes = kGroupLanes) {
+    const uint32_t per = split ? 2 * group_lanes : group_lanes;
     int kr = (int)((max_read_len + per - 1) / per);
     return kr < 1 ? 1 : kr;
 }
+
+// Pairs one wave scores: two per group (pairs layout) or one (split).
+__host__ __device__ inline uint32_t pairs_per_wave(bool split, uint32_t groups) { return split ? groups : 2 * groups; }
 
 // 16-byte vector loads of the window rows are legal.
 inline uint32_t vec_ok(const void* base, uint64_t stride) {
     return (stride % 16 == 0 && ((uintptr_t)base & 15) == 0) ? 1u : 0u;
 }
 
-// Dynamic LDS bytes for one 64-lane block.
-inline size_t lds_bytes(uint32_t lds_stride) { return 4u * (size_t)lds_stride * sizeof(uint32_t); }
+// Dynamic LDS bytes for one 64-lane block (one window stream per group).
+inline size_t lds_bytes(uint32_t lds_stride, uint32_t groups) {
+    return (size_t)groups * lds_stride * sizeof(uint32_t);
+}
 
 enum class Layout { kPairs, kSplit, kMixed };
 

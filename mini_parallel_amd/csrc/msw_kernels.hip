@@ -10,14 +10,16 @@
 //
 // Design (DESIGN.md has the derivation and the roofline):
 //  - Integer max-plus DP, VALU-bound: no MFMA, no LDS tiling of the matrix.
-//  - One wave64 = 4 lane groups of 16 (one DPP row each).  A group scores TWO
-//    pairs at once: pair "a" in the low 16 bits and pair "b" in the high 16
-//    bits of every register, so each packed-u16 VALU op updates two cells.
+//  - One wave64 = 64 / G lane groups of G lanes (G = 8..16, chosen per launch
+//    so the batch fills the SIMDs evenly).  A group scores TWO pairs at once:
+//    pair "a" in the low 16 bits and pair "b" in the high 16 bits of every
+//    register, so each packed-u16 VALU op updates two cells.
 //  - Lane l of a group owns read rows [l*KR, l*KR+KR) in VGPRs and sweeps the
 //    window with a one-column skew per lane (anti-diagonal wavefront): at step
 //    t lane l scores column t-l, reading that column's packed window code from
-//    an LDS stream.  Lane l-1's bottom-row values enter through DPP row_shr:1
-//    with bound_ctrl zero fill, which is the zero top boundary for lane 0.
+//    an LDS stream.  Lane l-1's bottom-row H enters through one
+//    v_and_b32_dpp wave_shr:1 whose mask zeroes each group's first lane: the
+//    zero top boundary.
 //  - Cell values are small non-negative integers kept as u16; the three-way max
 //    runs as v_pk_maximum3_f16 on their (denormal, ordered) f16 bit patterns,
 //    and the zero floor comes from u16 saturating subtracts.
@@ -64,10 +66,12 @@ __device__ __forceinline__ uint32_t track_max3(uint32_t best, uint32_t a, uint32
     return d;
 }
 
-// DPP row_shr:1 inside each 16-lane row; lane 0 of the row reads 0 (bound_ctrl),
-// which is exactly the matrix's zero top boundary for E, F, G and H.
-__device__ __forceinline__ uint32_t shr1_zero(uint32_t src) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src, 0x111, 0xF, 0xF, true);
+// Hand-off from lane l-1: DPP wave_shr:1 over the whole wave (lane 0 reads 0
+// through bound_ctrl), then top_mask zeroes the first lane of every group --
+// the matrix's zero top boundary for H and F.  hipcc folds the pair into one
+// v_and_b32_dpp.
+__device__ __forceinline__ uint32_t shr1_group(uint32_t src, uint32_t top_mask) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src, 0x138, 0xF, 0xF, true) & top_mask;
 }
 
 // Packed (H + match): a full-rate v_add_u32 suffices -- each u16 half stays
@@ -79,15 +83,15 @@ __device__ __forceinline__ uint32_t hi_to_lo_own_lo_to_hi(uint32_t own, uint32_t
     return __builtin_amdgcn_alignbit(own, dpp, 16);
 }
 
-// Lane-group layouts (template flag SPLIT):
-//  pairs (SPLIT = false): a 16-lane group scores two pairs, pair a in the low
-//      and pair b in the high u16 half; lane l owns rows [l*KR, l*KR+KR) of
-//      both and scores column t - l at step t.  8 pairs per wave.
-//  split (SPLIT = true): a 16-lane group scores one pair; lane l owns rows
+// Lane-group layouts (template flag SPLIT), G lanes per group:
+//  pairs (SPLIT = false): a group scores two pairs, pair a in the low and pair
+//      b in the high u16 half; lane l owns rows [l*KR, l*KR+KR) of both and
+//      scores column t - l at step t.  2 * (64 / G) pairs per wave.
+//  split (SPLIT = true): a group scores one pair; lane l owns rows
 //      [2l*KR, 2l*KR+KR) in the low half and the next KR rows in the high
 //      half, which runs one column behind: low half column t - 2l, high half
-//      t - 2l - 1.  4 pairs per wave: half the work per wave, for batches too
-//      small to give every SIMD two 8-pair waves.
+//      t - 2l - 1.  64 / G pairs per wave: half the work per wave, for batches
+//      too small to give every SIMD two pairs-waves.
 struct PairMeta {
     uint32_t pa, pb;  // pair indices (the same pair twice in the split layout)
     bool va, vb;
@@ -95,16 +99,16 @@ struct PairMeta {
 };
 
 template <bool SPLIT>
-__device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t block) {
+__device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t block, bool active) {
     // Branch-free: clamped indices keep every load legal (n_slots >= 1), the
-    // lengths of padding slots are masked to 0 afterwards.
+    // lengths of padding slots (and of idle lanes) are masked to 0 afterwards.
     PairMeta q;
-    const uint32_t slot_a = SPLIT ? block * 4u + g : block * 8u + 2u * g;
+    const uint32_t slot_a = block * pairs_per_wave(SPLIT, p.groups) + (SPLIT ? g : 2u * g);
     const uint32_t slot_b = SPLIT ? slot_a : slot_a + 1;
     const uint32_t last = p.n_slots - 1;
     const uint32_t sa = min(slot_a, last), sb = min(slot_b, last);
-    q.va = slot_a < p.n_slots;
-    q.vb = slot_b < p.n_slots;
+    q.va = active && slot_a < p.n_slots;
+    q.vb = active && slot_b < p.n_slots;
     q.pa = p.order ? p.order[sa] : p.slot_base + sa;
     q.pb = SPLIT ? q.pa : (p.order ? p.order[sb] : p.slot_base + sb);
     const int ma = p.read_len[q.pa], na = p.win_len[q.pa];
@@ -134,22 +138,22 @@ __device__ __forceinline__ uint32_t wcode(uint32_t byte, bool valid, uint32_t sh
 // (unaligned batches): byte loads with clamped addresses, no branches.
 template <bool SPLIT>
 __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& q, uint32_t* stream,
-                                             int steps, int lg) {
+                                             int steps, int lg, int G, bool active) {
+    if (!active) return;
     const uint8_t* wa = p.wins + (uint64_t)q.pa * p.win_stride;
     const uint8_t* wb = p.wins + (uint64_t)q.pb * p.win_stride;
     const uint32_t sh = p.code_shift;
     const int last = (int)p.win_stride - 1;
-    stream[lg] = kWinSentinel2;
-    stream[lg + kGroupLanes] = kWinSentinel2;
+    for (int k = lg; k < kLead; k += G) stream[k] = kWinSentinel2;
     const int nch = (steps + 15) >> 4;  // chunks of 16 columns to stage
     if (p.win_vec) {
         const int loadable = (int)(p.win_stride >> 4);
-        for (int k0 = 0; k0 < nch; k0 += 4 * kGroupLanes) {
+        for (int k0 = 0; k0 < nch; k0 += 4 * G) {
             uint4 va[4], vb[4];
             uint32_t prev[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int k = k0 + u * kGroupLanes + lg;
+                const int k = k0 + u * G + lg;
                 const bool ld = k < nch && k < loadable;
                 va[u] = ld ? *reinterpret_cast<const uint4*>(wa + 16 * k) : make_uint4(0, 0, 0, 0);
                 if constexpr (SPLIT) {
@@ -160,7 +164,7 @@ __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& 
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int k = k0 + u * kGroupLanes + lg;
+                const int k = k0 + u * G + lg;
                 if (k < nch) {
                     const uint32_t xa[4] = {va[u].x, va[u].y, va[u].z, va[u].w};
                     uint32_t xb[4] = {0u, 0u, 0u, 0u};
@@ -189,17 +193,17 @@ __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& 
             }
         }
     } else {
-        for (int c0 = 0; c0 < steps; c0 += 4 * kGroupLanes) {
+        for (int c0 = 0; c0 < steps; c0 += 4 * G) {
             uint32_t ba[4], bb[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int c = c0 + u * kGroupLanes + lg;
+                const int c = c0 + u * G + lg;
                 ba[u] = wa[min(c, last)];
                 bb[u] = SPLIT ? wa[min(max(c - 1, 0), last)] : wb[min(c, last)];
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int c = c0 + u * kGroupLanes + lg;
+                const int c = c0 + u * G + lg;
                 const bool vb = SPLIT ? (c >= 1 && c - 1 < q.na) : (c < q.nb);
                 if (c < steps) stream[kLead + c] = wcode(ba[u], c < q.na, sh) | (wcode(bb[u], vb, sh) << 16);
             }
@@ -233,20 +237,27 @@ __device__ __forceinline__ void load_read_codes(const SwParams& p, const PairMet
     }
 }
 
-__device__ __forceinline__ uint32_t group_pk_max(uint32_t v) {
+// Reductions over a group's G lanes into its first lane: a tree clipped at the
+// group's end (lane lg gathers [lg, min(lg + 2^k, G)) after step k).
+__device__ __forceinline__ uint32_t group_pk_max(uint32_t v, int lg, int G) {
+    const int lane = threadIdx.x;
 #pragma unroll
-    for (int off = 8; off > 0; off >>= 1) v = pk_max(v, (uint32_t)__shfl_xor((int)v, off, kGroupLanes));
+    for (int off = 1; off < 16; off <<= 1) {
+        const uint32_t o = (uint32_t)__shfl((int)v, lane + off, 64);
+        v = lg + off < G ? pk_max(v, o) : v;
+    }
     return v;
 }
 
 // Best-cell key: score in the high word, (0xFFFF - i, 0xFFFF - j) in the low
 // word, so the max key is max score, then smallest i, then smallest j -- the
 // oracle's row-major scan with strict '>'.
-__device__ __forceinline__ uint64_t group_max_u64(uint64_t v) {
+__device__ __forceinline__ uint64_t group_max_u64(uint64_t v, int lg, int G) {
+    const int lane = threadIdx.x;
 #pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(v, off, kGroupLanes);
-        v = o > v ? o : v;
+    for (int off = 1; off < 16; off <<= 1) {
+        const uint64_t o = __shfl(v, lane + off, 64);
+        v = (lg + off < G && o > v) ? o : v;
     }
     return v;
 }
@@ -269,7 +280,7 @@ __device__ __forceinline__ void store_hit(const SwParams& p, bool valid, uint32_
 
 // Per-row keys (h << 16 | 0xFFFF - j, one per u16 half) -> best hits.
 template <int KR, bool SPLIT>
-__device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta& q, int lg,
+__device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta& q, int lg, int G,
                                               const uint32_t (&key_a)[KR], const uint32_t (&key_b)[KR],
                                               uint32_t bias) {
     uint64_t ga = 0, gb = 0;
@@ -286,11 +297,11 @@ __device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta&
     }
     if constexpr (SPLIT) {
         ga = gb > ga ? gb : ga;
-        ga = group_max_u64(ga);
+        ga = group_max_u64(ga, lg, G);
         if (lg == 0) store_hit(p, q.va, q.pa, ga, bias);
     } else {
-        ga = group_max_u64(ga);
-        gb = group_max_u64(gb);
+        ga = group_max_u64(ga, lg, G);
+        gb = group_max_u64(gb, lg, G);
         if (lg == 0) {
             store_hit(p, q.va, q.pa, ga, bias);
             store_hit(p, q.vb, q.pb, gb, bias);
@@ -299,9 +310,9 @@ __device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta&
 }
 
 template <bool SPLIT>
-__device__ __forceinline__ void finish_score(const SwParams& p, const PairMeta& q, int lg, uint32_t best,
-                                             uint32_t bias) {
-    best = group_pk_max(best);
+__device__ __forceinline__ void finish_score(const SwParams& p, const PairMeta& q, int lg, int G,
+                                             uint32_t best, uint32_t bias) {
+    best = group_pk_max(best, lg, G);
     if (lg == 0) {
         if constexpr (SPLIT) {
             store_score(p, q.va, q.pa, max(best & 0xFFFFu, best >> 16) - bias);
@@ -316,8 +327,8 @@ __device__ __forceinline__ void finish_score(const SwParams& p, const PairMeta& 
 // boundary).  Split layout: the low half takes lane l-1's high-half row, the
 // high half takes this lane's own low-half row of the previous step.
 template <bool SPLIT>
-__device__ __forceinline__ uint32_t from_above(uint32_t own_bottom) {
-    const uint32_t d = shr1_zero(own_bottom);
+__device__ __forceinline__ uint32_t from_above(uint32_t own_bottom, uint32_t top_mask) {
+    const uint32_t d = shr1_group(own_bottom, top_mask);
     if constexpr (SPLIT) return hi_to_lo_own_lo_to_hi(own_bottom, d);
     else return d;
 }
@@ -361,14 +372,15 @@ __device__ __forceinline__ uint32_t row_table(uint32_t v, uint32_t shift, uint32
 // Checks this lane's share of the group's staged window stream; returns true
 // (wave-uniform) if every window byte of the wave is A/C/G/T, and then
 // rewrites the stream in place as selectors.  Reads may hold any byte.
-__device__ __forceinline__ bool to_fast_path(uint32_t* stream, int words, int lg, uint32_t shift) {
+__device__ __forceinline__ bool to_fast_path(uint32_t* stream, int words, int lg, int G, bool active,
+                                             uint32_t shift) {
     bool ok = true;
-    for (int k = lg; k < words; k += kGroupLanes) {
+    for (int k = lg; active && k < words; k += G) {
         const uint32_t w = stream[k];
         ok = ok && code_ok(w & 0xFFFFu, shift) && code_ok(w >> 16, shift);
     }
     if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
-    for (int k = lg; k < words; k += kGroupLanes) stream[k] = win_selector(stream[k], shift);
+    for (int k = lg; active && k < words; k += G) stream[k] = win_selector(stream[k], shift);
     __syncthreads();
     return true;
 }
@@ -391,13 +403,23 @@ __device__ __forceinline__ bool to_fast_path(uint32_t* stream, int words, int lg
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
 __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint32_t* lds) {
     const int lane = threadIdx.x;
-    const int g = lane >> 4, lg = lane & 15;
-    const PairMeta q = load_meta<SPLIT>(p, g, block);
-    const int skew = SPLIT ? 2 * (kGroupLanes - 1) + 1 : kGroupLanes - 1;
+    const int G = (int)p.group_lanes;
+    const int g_raw = lane / G;
+    // Lanes past groups * G idle: they run the loop on group 0's stream with
+    // empty pairs and write nothing.
+    const bool active = g_raw < (int)p.groups;
+    const int g = active ? g_raw : 0;
+    const int lg = active ? lane - g_raw * G : 0;
+    // An opaque all-ones / zero word (not a bool), so the AND after the DPP
+    // move folds into one v_and_b32_dpp instead of becoming a v_cndmask.
+    uint32_t top_mask = lg == 0 ? 0u : ~0u;
+    asm volatile("" : "+v"(top_mask));
+    const PairMeta q = load_meta<SPLIT>(p, g, block, active);
+    const int skew = SPLIT ? 2 * (G - 1) + 1 : G - 1;
     // wavefront steps, rounded up to even for the two-step unrolled loop
     const int steps = (__builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + skew + 1) & ~1;
     uint32_t* stream = lds + g * p.lds_stride;
-    stage_window<SPLIT>(p, q, stream, steps, lg);
+    stage_window<SPLIT>(p, q, stream, steps, lg, G, active);
     uint32_t rc[KR];
     load_read_codes<KR, SPLIT>(p, q, lg, rc);
     __syncthreads();
@@ -461,12 +483,12 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
             // the bias is re-added on arrival: no u16 half ever goes negative.
             // Only H (and affine F) cross: E resp. GK of the row above are
             // functions of its H, recomputed here instead of a second DPP move.
-            const uint32_t h_up = from_above<SPLIT>(h_bot - bias2);
+            const uint32_t h_up = from_above<SPLIT>(h_bot - bias2, top_mask);
             const uint32_t d_up = add_nc(h_up, kmatch2);
             uint32_t up;    // linear: E of the row above; affine: F* of the row above
             uint32_t g_up;  // affine: GK of the row above
             if constexpr (AFFINE) {
-                up = add_nc(from_above<SPLIT>(f_bot - bias2), bias2);
+                up = add_nc(from_above<SPLIT>(f_bot - bias2, top_mask), bias2);
                 g_up = add_nc(pk_satsub(h_up, og2), bias2);
             } else {
                 up = pk_satsub(h_up, ext2);
@@ -529,12 +551,12 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     };
     // Words of the group's stream the loop consumes (all staged).
     const int words = kLead + steps;
-    const bool fast = to_fast_path(stream, words, lg, p.code_shift);
+    const bool fast = to_fast_path(stream, words, lg, G, active, p.code_shift);
     if (fast) run(std::true_type{});
     else run(std::false_type{});
 
-    if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, key_a, key_b, bias2 & 0xFFFFu);
-    else finish_score<SPLIT>(p, q, lg, best, bias2 & 0xFFFFu);
+    if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, G, key_a, key_b, bias2 & 0xFFFFu);
+    else finish_score<SPLIT>(p, q, lg, G, best, bias2 & 0xFFFFu);
     return fast;
 }
 
@@ -592,7 +614,7 @@ __global__ __launch_bounds__(64) void sw_mixed_kernel(SwParams p) {
         trace_end(p, wc, fast, false, KRP);
     } else {
         SwParams q = p;
-        const uint32_t done = p.pairs_blocks * (uint32_t)kPairsPerWave;
+        const uint32_t done = p.pairs_blocks * pairs_per_wave(false, p.groups);
         q.n_slots = p.n_slots - done;
         q.order = p.order ? p.order + done : nullptr;
         if (!p.order) q.slot_base = done;
@@ -639,9 +661,9 @@ __global__ __launch_bounds__(256) void sw_compat_kernel(const uint8_t* __restric
 // ---------------------------------------------------------------------------
 template <int KR, bool SPLIT>
 static hipError_t launch_kr(const SwParams& p, bool affine, bool coords, hipStream_t stream) {
-    const uint32_t per_wave = SPLIT ? 4u : (uint32_t)kPairsPerWave;
+    const uint32_t per_wave = pairs_per_wave(SPLIT, p.groups);
     const dim3 grid((p.n_slots + per_wave - 1) / per_wave), block(64);
-    const size_t shm = lds_bytes(p.lds_stride);
+    const size_t shm = lds_bytes(p.lds_stride, p.groups);
     if (affine) {
         if (coords) hipLaunchKernelGGL((sw_kernel<KR, true, true, SPLIT>), grid, block, shm, stream, p);
         else hipLaunchKernelGGL((sw_kernel<KR, true, false, SPLIT>), grid, block, shm, stream, p);
@@ -655,7 +677,7 @@ static hipError_t launch_kr(const SwParams& p, bool affine, bool coords, hipStre
 template <int KRP>
 static hipError_t launch_mixed_kr(const SwParams& p, bool affine, bool coords, uint32_t blocks,
                                   hipStream_t stream) {
-    const size_t shm = lds_bytes(p.lds_stride);
+    const size_t shm = lds_bytes(p.lds_stride, p.groups);
     if (affine) {
         if (coords) hipLaunchKernelGGL((sw_mixed_kernel<KRP, true, true>), dim3(blocks), dim3(64), shm, stream, p);
         else hipLaunchKernelGGL((sw_mixed_kernel<KRP, true, false>), dim3(blocks), dim3(64), shm, stream, p);
@@ -670,9 +692,9 @@ hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_r
                      hipStream_t stream) {
     if (p.n_slots == 0) return hipSuccess;
     if (layout == Layout::kMixed) {
-        const uint32_t rest = p.n_slots - min(p.n_slots, p.pairs_blocks * (uint32_t)kPairsPerWave);
-        const uint32_t blocks = p.pairs_blocks + (rest + 3) / 4;
-        switch (rows_per_lane(max_read_len, false)) {
+        const uint32_t rest = p.n_slots - min(p.n_slots, p.pairs_blocks * pairs_per_wave(false, p.groups));
+        const uint32_t blocks = p.pairs_blocks + (rest + p.groups - 1) / p.groups;
+        switch (rows_per_lane(max_read_len, false, p.group_lanes)) {
             case 2: return launch_mixed_kr<2>(p, affine, coords, blocks, stream);
             case 4: return launch_mixed_kr<4>(p, affine, coords, blocks, stream);
             case 6: return launch_mixed_kr<6>(p, affine, coords, blocks, stream);
@@ -686,7 +708,7 @@ hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_r
     }
     const bool split = layout == Layout::kSplit;
     if (split) {
-        switch (rows_per_lane(max_read_len, true)) {
+        switch (rows_per_lane(max_read_len, true, p.group_lanes)) {
             case 1: return launch_kr<1, true>(p, affine, coords, stream);
             case 2: return launch_kr<2, true>(p, affine, coords, stream);
             case 3: return launch_kr<3, true>(p, affine, coords, stream);
@@ -698,7 +720,7 @@ hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_r
             default: return hipErrorInvalidValue;
         }
     }
-    switch (rows_per_lane(max_read_len, false)) {
+    switch (rows_per_lane(max_read_len, false, p.group_lanes)) {
         case 1: return launch_kr<1, false>(p, affine, coords, stream);
         case 2: return launch_kr<2, false>(p, affine, coords, stream);
         case 3: return launch_kr<3, false>(p, affine, coords, stream);

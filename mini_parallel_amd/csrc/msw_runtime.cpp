@@ -240,55 +240,105 @@ uint64_t default_chunk() {
     return 65536;
 }
 
-// Lane-group layout for one launch (msw_kernels.hip): "pairs" packs two pairs
-// per 16-lane group (8 per wave, least work per cell), "split" gives one pair
-// per group (4 per wave, ~10 % more work per cell, half the work per wave),
-// "mixed" runs up to one pairs-wave per SIMD and the rest as split-waves.
-// The choice minimises a makespan model: waves are dealt round-robin over the
-// 4 x CU SIMDs in block order, a wave costs steps x instructions per step
-// (7.3 per packed row; tools/ubench_valu.hip and profiles/ for the numbers),
-// and a SIMD's time is the sum of its waves' costs.
-// MSW_LAYOUT=pairs|split|mixed overrides (tests use it to cover every path).
+// Lane-group layout of one launch.  "pairs" scores 2 pairs per G-lane group,
+// "split" 1 pair per group (rows split over the two halves; half the work per
+// wave), "mixed" (G = 16) runs up to one pairs-wave per SIMD and the rest as
+// split-waves.  G (8..16 lanes per group, 64 / G groups per wave) sets how many
+// pairs one wave holds, so a small batch can be cut into about one wave per
+// SIMD.  The choice minimises a makespan model:
+//  - a wave issues steps x (a * KR + b) instructions (a, b fitted to the
+//    compiled loops: tools/issue_sim.py);
+//  - waves are dealt round-robin over the 4 x CU SIMDs in block order (what
+//    tools/wave_trace.py observes), and a SIMD holding k waves issues one
+//    instruction per r(k) cycles (measured: 5.27 alone, 4.6 for two, 3.94 at
+//    eight -- a lone wave cannot issue back to back).
+// MSW_LAYOUT=pairs|split|mixed and MSW_GROUP_LANES=8..16 override (tests use
+// them to cover every path).
 struct LaunchPlan {
     msw::Layout layout;
     uint32_t pairs_blocks;
+    uint32_t group_lanes;
+    uint32_t groups;
 };
 
+static double simd_cycles_per_instr(uint64_t k) {
+    static const double r[] = {0.0, 5.27, 4.6, 4.3, 4.15, 4.05, 4.0, 3.97, 3.94};
+    return r[k > 8 ? 8 : k];
+}
+
 LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const Scheme& sch, int cu_count) {
-    const int krp = msw::rows_per_lane(max_m, false);
-    const bool mixed_ok = (krp % 2) == 0;
     const uint64_t simds = 4ull * (uint64_t)(cu_count > 0 ? cu_count : 256);
-    double row = 7.3;
-    if (sch.affine) row = 12.5;
-    if (sch.coords) row += 3.0;
-    const double cost_p = (max_n + 15.0) * (krp * row + 5.0);
-    const double cost_s = (max_n + 31.0) * (msw::rows_per_lane(max_m, true) * row + 10.0);
-    auto makespan = [&](uint64_t pairs_waves, uint64_t split_waves) {
-        std::vector<double> load(simds, 0.0);
-        for (uint64_t i = 0; i < pairs_waves; ++i) load[i % simds] += cost_p;
-        for (uint64_t i = pairs_waves; i < pairs_waves + split_waves; ++i) load[i % simds] += cost_s;
-        return *std::max_element(load.begin(), load.end());
+    const double per_row = 5.5 + (sch.affine ? 5.2 : 0.0) + (sch.coords ? 2.8 : 0.0);
+    auto wave_instr = [&](bool split, uint32_t G) {
+        const int kr = msw::rows_per_lane(max_m, split, G);
+        const double steps = (double)max_n + (split ? 2.0 * G : (double)G);
+        const double over = (split ? 5.5 : 3.0) + (sch.affine ? 2.0 : 0.0);
+        return steps * (per_row * kr + over) + 300.0;
     };
-    const uint64_t all_p = (n_pairs + 7) / 8, all_s = (n_pairs + 3) / 4;
-    LaunchPlan best{msw::Layout::kPairs, 0};
-    double best_t = makespan(all_p, 0);
-    const double t_s = makespan(0, all_s);
-    if (t_s < best_t) { best_t = t_s; best = {msw::Layout::kSplit, 0}; }
-    if (mixed_ok && all_p > simds / 4) {
+    // Round-robin dealing: SIMD i holds waves i, i + S, ...; time = its
+    // instructions x r(its wave count).
+    auto makespan = [&](uint64_t w1, double c1, uint64_t w2, double c2) {
+        const uint64_t w = w1 + w2;
+        if (w == 0) return 0.0;
+        if (w2 == 0 || w1 == 0) {
+            const double c = w1 ? c1 : c2;
+            const uint64_t k = (w + simds - 1) / simds;
+            return (double)k * c * simd_cycles_per_instr(k);
+        }
+        std::vector<double> load(simds, 0.0);
+        std::vector<uint32_t> cnt(simds, 0);
+        for (uint64_t i = 0; i < w; ++i) {
+            load[i % simds] += i < w1 ? c1 : c2;
+            cnt[i % simds]++;
+        }
+        double t = 0.0;
+        for (uint64_t i = 0; i < simds; ++i) t = std::max(t, load[i] * simd_cycles_per_instr(cnt[i]));
+        return t;
+    };
+    const uint32_t stride = msw::stream_stride(max_n);
+    const char* env_g = getenv("MSW_GROUP_LANES");
+    const uint32_t force_g = env_g ? (uint32_t)atoi(env_g) : 0u;
+    const char* env = getenv("MSW_LAYOUT");
+    const bool force_pairs = env && !strcmp(env, "pairs"), force_split = env && !strcmp(env, "split");
+    const bool force_mixed = env && !strcmp(env, "mixed");
+
+    LaunchPlan best{msw::Layout::kPairs, 0, 16, 4};
+    double best_t = 1e300;
+    for (int split = 0; split <= 1; ++split) {
+        if ((force_pairs && split) || (force_split && !split) || force_mixed) continue;
+        for (uint32_t G = 16; G >= 8; --G) {
+            if (force_g ? G != force_g : ((force_pairs || force_split) && G != 16)) continue;
+            const int kr = msw::rows_per_lane(max_m, split, G);
+            if (kr > (split ? 8 : 16)) continue;
+            const uint32_t groups = 64 / G;
+            if (G != 16 && msw::lds_bytes(stride, groups) > 65536) continue;
+            const uint64_t per = msw::pairs_per_wave(split, groups);
+            const double t = makespan((n_pairs + per - 1) / per, wave_instr(split, G), 0, 0.0);
+            if (t < best_t * 0.995) {
+                best_t = t;
+                best = {split ? msw::Layout::kSplit : msw::Layout::kPairs, 0, G, groups};
+            }
+        }
+    }
+    // Mixed grid (G = 16, even KR): up to one pairs-wave per SIMD, then split waves.
+    const int krp = msw::rows_per_lane(max_m, false);
+    const bool mixed_ok = (krp % 2) == 0 && (!force_g || force_g == 16) && !force_pairs && !force_split;
+    if (mixed_ok) {
+        const double cp = wave_instr(false, 16), cs = wave_instr(true, 16);
         for (uint64_t k = 1; k <= 4; ++k) {
             const uint64_t pw = std::min<uint64_t>(n_pairs / 8, k * simds / 4);
             if (pw == 0) continue;
             const uint64_t rest = n_pairs - pw * 8;
-            const double t = makespan(pw, (rest + 3) / 4);
-            if (t < best_t * 0.995) { best_t = t; best = {msw::Layout::kMixed, (uint32_t)pw}; }
+            const double t = makespan(pw, cp, (rest + 3) / 4, cs);
+            if (t < best_t * 0.995 || (force_mixed && best.layout != msw::Layout::kMixed)) {
+                best_t = t;
+                best = {msw::Layout::kMixed, (uint32_t)pw, 16, 4};
+            }
         }
-    }
-    const char* env = getenv("MSW_LAYOUT");
-    if (env && !strcmp(env, "pairs")) best = {msw::Layout::kPairs, 0};
-    if (env && !strcmp(env, "split")) best = {msw::Layout::kSplit, 0};
-    if (env && !strcmp(env, "mixed")) {
-        if (mixed_ok) best = {msw::Layout::kMixed, (uint32_t)std::min<uint64_t>(n_pairs / 8, simds)};
-        else best = {msw::Layout::kSplit, 0};
+        if (force_mixed && best.layout != msw::Layout::kMixed)
+            best = {msw::Layout::kMixed, (uint32_t)std::min<uint64_t>(n_pairs / 8, simds), 16, 4};
+    } else if (force_mixed) {
+        best = {msw::Layout::kSplit, 0, 16, 4};
     }
     return best;
 }
@@ -346,6 +396,8 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.win_vec = msw::vec_ok(p.wins, p.win_stride);
         const LaunchPlan plan = choose_layout(b.count, b.max_m, b.max_n, sch, ctx->cu_count);
         p.pairs_blocks = plan.pairs_blocks;
+        p.group_lanes = plan.group_lanes;
+        p.groups = plan.groups;
         HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan.layout, ctx->compute));
     }
     (void)n;
@@ -563,7 +615,8 @@ int msw_wait(msw_ctx* ctx, uint64_t ticket) {
 
 // Diagnostics only (MSW_WAVE_TRACE=file, read by tools/wave_trace.py): the
 // launch records per-block clocks and placement and appends one record
-// {u64 n_blocks, u64 layout, n_blocks x 4 u64} to the file.  Synchronous.
+// {u64 n_blocks, u64 layout | G << 8 | pairs_blocks << 16, n_blocks x 4 u64}
+// to the file.  Synchronous.
 static int traced_launch(msw::SwParams p, const Scheme& sch, uint32_t max_read_len, const LaunchPlan& plan,
                          hipStream_t st, const char* path) {
     const uint64_t n_blocks = p.n_slots / 4 + 2;  // the split layout's count bounds every grid
@@ -579,7 +632,8 @@ static int traced_launch(msw::SwParams p, const Scheme& sch, uint32_t max_read_l
     if (e != hipSuccess) return fail(MSW_E_DEVICE, "traced launch: %s", hipGetErrorString(e));
     FILE* f = fopen(path, "ab");
     if (!f) return fail(MSW_E_INVALID, "cannot open MSW_WAVE_TRACE file %s", path);
-    const uint64_t hdr[2] = {n_blocks, (uint64_t)plan.layout | ((uint64_t)plan.pairs_blocks << 8)};
+    const uint64_t hdr[2] = {n_blocks, (uint64_t)plan.layout | ((uint64_t)plan.group_lanes << 8) |
+                                           ((uint64_t)plan.pairs_blocks << 16)};
     fwrite(hdr, sizeof(hdr), 1, f);
     fwrite(h.data(), sizeof(uint64_t), h.size(), f);
     fclose(f);
@@ -615,6 +669,8 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
     const LaunchPlan plan = choose_layout(b->n_pairs, max_read_len, max_win_len, sch, ctx->cu_count);
     p.pairs_blocks = plan.pairs_blocks;
+    p.group_lanes = plan.group_lanes;
+    p.groups = plan.groups;
     const char* trace_path = getenv("MSW_WAVE_TRACE");
     if (trace_path && *trace_path) return traced_launch(p, sch, max_read_len, plan, st, trace_path);
     HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st));

@@ -37,11 +37,19 @@ def assert_same(got, want, coords: bool):
                                f"{list(zip(i[bad[:5]], j[bad[:5]]))} oracle {list(zip(wi[bad[:5]], wj[bad[:5]]))}")
 
 
-@pytest.fixture(params=["pairs", "split", "mixed"])
+@pytest.fixture(params=["pairs", "split", "mixed", "pairs:12", "pairs:9", "pairs:8", "split:11", "split:8"])
 def layout(request, monkeypatch):
-    """Both lane-group layouts of the kernel (the runtime normally picks one
-    per launch from a makespan model)."""
-    monkeypatch.setenv("MSW_LAYOUT", request.param)
+    """Every lane-group layout of the kernel, with 16-lane groups and with
+    narrower ones (G = 12, 11, 9, 8: idle lanes at the wave's end, groups that
+    straddle DPP rows).  The runtime normally picks layout and G per launch
+    from a makespan model; a forced G that cannot hold the batch's reads
+    (KR > 16, or the LDS budget) falls back to G = 16."""
+    lay, _, g = request.param.partition(":")
+    monkeypatch.setenv("MSW_LAYOUT", lay)
+    if g:
+        monkeypatch.setenv("MSW_GROUP_LANES", g)
+    else:
+        monkeypatch.delenv("MSW_GROUP_LANES", raising=False)
     return request.param
 
 

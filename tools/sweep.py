@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--affine", action="store_true")
     ap.add_argument("--coords", action="store_true")
+    ap.add_argument("--group-lanes", default="0", help="comma list of forced G (0 = runtime choice)")
     args = ap.parse_args()
 
     import numpy as np
@@ -44,10 +45,15 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     for layout in args.layouts.split(","):
+      for gl in args.group_lanes.split(","):
         if layout == "auto":
             os.environ.pop("MSW_LAYOUT", None)
         else:
             os.environ["MSW_LAYOUT"] = layout
+        if int(gl):
+            os.environ["MSW_GROUP_LANES"] = gl
+        else:
+            os.environ.pop("MSW_GROUP_LANES", None)
         for n in sizes:
             cells = int((b.read_len[:n].astype(np.int64) * b.win_len[:n]).sum())
             step = ctx.prepare_device_launch(reads.data_ptr(), rl.data_ptr(), wins.data_ptr(), wl.data_ptr(),
@@ -63,7 +69,7 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
-            print(json.dumps({"layout": layout, "pairs": n, "ms": round(ms, 4),
+            print(json.dumps({"layout": layout, "G": int(gl), "pairs": n, "ms": round(ms, 4),
                               "gcups": round(cells / ms / 1e6, 1)}), flush=True)
 
 

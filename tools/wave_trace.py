@@ -33,7 +33,7 @@ def decode(path):
     while k < raw.size:
         n, lay = int(raw[k]), int(raw[k + 1])
         blk = raw[k + 2:k + 2 + 4 * n].reshape(n, 4)
-        recs.append((lay & 0xFF, lay >> 8, blk))
+        recs.append((lay & 0xFF, (lay >> 8) & 0xFF, lay >> 16, blk))
         k += 2 + 4 * n
     return recs
 
@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=10000)
     ap.add_argument("--layout", default="auto")
+    ap.add_argument("--group-lanes", type=int, default=0)
     ap.add_argument("--affine", action="store_true")
     ap.add_argument("--coords", action="store_true")
     ap.add_argument("--dump", default="")
@@ -101,6 +102,8 @@ def main():
 
     if args.layout != "auto":
         os.environ["MSW_LAYOUT"] = args.layout
+    if args.group_lanes:
+        os.environ["MSW_GROUP_LANES"] = str(args.group_lanes)
     b = config_batch(args.config, n_pairs=args.pairs)
     dev = torch.device("cuda", 0)
     reads = torch.from_numpy(b.reads).to(dev)
@@ -130,13 +133,13 @@ def main():
     recs = decode(path)
     os.unlink(path)
     res = []
-    for lay, pb, blk in recs:
+    for lay, g, pb, blk in recs:
         s = summarise(blk)
-        s.update({"layout": LAYOUTS.get(lay, lay), "pairs_blocks": pb, "pairs": b.n_pairs})
+        s.update({"layout": LAYOUTS.get(lay, lay), "group_lanes": g, "pairs_blocks": pb, "pairs": b.n_pairs})
         res.append(s)
         print(json.dumps(s), flush=True)
     if args.dump:
-        np.save(args.dump, recs[-1][2])
+        np.save(args.dump, recs[-1][3])
 
 
 if __name__ == "__main__":
