@@ -53,7 +53,22 @@ struct SwParams {
     uint64_t* trace;          // diagnostics (MSW_WAVE_TRACE): 4 words per block, or nullptr
     uint32_t group_lanes;     // G: lanes per lane group (8..16)
     uint32_t groups;          // lane groups per wave = 64 / G (lanes past groups * G idle)
+    // f16 fast path (ACGT windows): cell values H * 2^-11 as packed f16.
+    uint32_t f16_ok;          // 1: the scheme and this launch's bound fit (msw_runtime.cpp)
+    uint32_t f16_hi;          // high byte of f16(+match) | high byte of f16(mismatch) << 8
+    uint32_t f16_ngap2;       // f16(-gap) (linear) / f16(-gap_extend) (affine), both halves
+    uint32_t f16_noe2;        // affine: f16(-(gap_open + gap_extend)), both halves
 };
+
+// f16 bits of the cell value v * 2^-11 (|v| < 2048: exact, normal or zero).
+inline uint32_t f16_cell_bits(int32_t v) {
+    if (v == 0) return 0u;
+    const uint32_t sign = v < 0 ? 0x8000u : 0u;
+    uint32_t a = (uint32_t)(v < 0 ? -v : v);
+    int e = 31 - __builtin_clz(a);  // a = 1.f * 2^e
+    const uint32_t mant = (a << (10 - e)) & 0x3FFu;
+    return sign | ((uint32_t)(e + 4) << 10) | mant;  // exponent bias 15, scale 2^-11
+}
 
 // Packed rows per lane for a read-length bound: ceil(m / 16) in the pairs
 // layout, ceil(m / 32) in the split layout (each packed row holds two rows).

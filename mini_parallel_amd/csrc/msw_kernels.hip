@@ -58,6 +58,25 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return __builtin_bit_cast(uint32_t,
                               __builtin_elementwise_maximum(x, __builtin_elementwise_maximum(y, z)));
 }
+// Packed f16 arithmetic of the fast path (cell values are H * 2^-11, exact).
+__device__ __forceinline__ uint32_t hadd(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, a) + __builtin_bit_cast(f16x2, b));
+}
+// a + b clamped to [0, 1]: one v_pk_add_f16 ... clamp (hipcc folds the min/max).
+__device__ __forceinline__ uint32_t hadd_clamp(uint32_t a, uint32_t b) {
+    const f16x2 z = {(_Float16)0.0f, (_Float16)0.0f}, one = {(_Float16)1.0f, (_Float16)1.0f};
+    const f16x2 v = __builtin_bit_cast(f16x2, a) + __builtin_bit_cast(f16x2, b);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_max(v, z), one));
+}
+__device__ __forceinline__ uint32_t hmax(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_bit_cast(f16x2, a),
+                                                                      __builtin_bit_cast(f16x2, b)));
+}
+// f16 cell value (H * 2^-11, H < 2048) -> integer score H.
+__device__ __forceinline__ uint32_t f16_to_score(uint32_t bits) {
+    return (uint32_t)((float)__builtin_bit_cast(_Float16, (unsigned short)bits) * 2048.0f);
+}
+
 // Score tracking max (opaque so the compiler keeps one op per two rows
 // instead of re-associating into a tree).
 __device__ __forceinline__ uint32_t track_max3(uint32_t best, uint32_t a, uint32_t b) {
@@ -134,7 +153,7 @@ __device__ __forceinline__ uint32_t wcode(uint32_t byte, bool valid, uint32_t sh
 //   pairs: stream[kLead + c] = code(win_a[c]) | code(win_b[c])   << 16
 //   split: stream[kLead + c] = code(win[c])   | code(win[c - 1]) << 16
 // Sentinels past each window.  Vector path: 16-byte loads, a round of up to
-// four chunks of 16 columns per lane in flight together.  Scalar path
+// two chunks of 16 columns per lane in flight together.  Scalar path
 // (unaligned batches): byte loads with clamped addresses, no branches.
 template <bool SPLIT>
 __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& q, uint32_t* stream,
@@ -148,11 +167,11 @@ __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& 
     const int nch = (steps + 15) >> 4;  // chunks of 16 columns to stage
     if (p.win_vec) {
         const int loadable = (int)(p.win_stride >> 4);
-        for (int k0 = 0; k0 < nch; k0 += 4 * G) {
-            uint4 va[4], vb[4];
-            uint32_t prev[4];
+        for (int k0 = 0; k0 < nch; k0 += 2 * G) {
+            uint4 va[2], vb[2];
+            uint32_t prev[2];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < 2; ++u) {
                 const int k = k0 + u * G + lg;
                 const bool ld = k < nch && k < loadable;
                 va[u] = ld ? *reinterpret_cast<const uint4*>(wa + 16 * k) : make_uint4(0, 0, 0, 0);
@@ -163,7 +182,7 @@ __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& 
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < 2; ++u) {
                 const int k = k0 + u * G + lg;
                 if (k < nch) {
                     const uint32_t xa[4] = {va[u].x, va[u].y, va[u].z, va[u].w};
@@ -211,15 +230,14 @@ __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& 
     }
 }
 
-// Read codes of this lane's packed rows.  Unconditional loads with clamped
-// addresses (all in flight at once), masked afterwards.
+// Read bytes of this lane's packed rows: unconditional loads with clamped
+// addresses (all in flight at once, issued before the pair lengths arrive).
 template <int KR, bool SPLIT>
-__device__ __forceinline__ void load_read_codes(const SwParams& p, const PairMeta& q, int lg,
-                                                uint32_t (&rc)[KR]) {
-    const uint8_t* ra = p.reads + (uint64_t)q.pa * p.read_stride;
-    const uint8_t* rb = p.reads + (uint64_t)q.pb * p.read_stride;
+__device__ __forceinline__ void load_read_bytes(const SwParams& p, uint32_t pa, uint32_t pb, int lg,
+                                                uint32_t (&ba)[KR], uint32_t (&bb)[KR]) {
+    const uint8_t* ra = p.reads + (uint64_t)pa * p.read_stride;
+    const uint8_t* rb = p.reads + (uint64_t)pb * p.read_stride;
     const int last = (int)p.read_stride - 1;
-    uint32_t ba[KR], bb[KR];
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
         const int ia = SPLIT ? lg * 2 * KR + r : lg * KR + r;
@@ -227,6 +245,13 @@ __device__ __forceinline__ void load_read_codes(const SwParams& p, const PairMet
         ba[r] = ra[min(ia, last)];
         bb[r] = rb[min(ib, last)];
     }
+}
+
+// Read codes (byte << code_shift, or the sentinel past the read) of this
+// lane's packed rows, pair a in the low and pair b in the high half.
+template <int KR, bool SPLIT>
+__device__ __forceinline__ void read_codes(const SwParams& p, const PairMeta& q, int lg, const uint32_t (&ba)[KR],
+                                           const uint32_t (&bb)[KR], uint32_t (&rc)[KR]) {
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
         const int ia = SPLIT ? lg * 2 * KR + r : lg * KR + r;
@@ -267,9 +292,9 @@ __device__ __forceinline__ void store_score(const SwParams& p, bool valid, uint3
 }
 
 __device__ __forceinline__ void store_hit(const SwParams& p, bool valid, uint32_t pair, uint64_t key,
-                                          uint32_t bias) {
+                                          uint32_t bias, bool f16) {
     if (!valid) return;
-    const uint32_t s = (uint32_t)(key >> 32) - bias;
+    const uint32_t s = f16 ? f16_to_score((uint32_t)(key >> 32)) : (uint32_t)(key >> 32) - bias;
     p.score[pair] = (int32_t)s;
     if (p.end_i) {
         const uint32_t lo = (uint32_t)key;
@@ -282,7 +307,7 @@ __device__ __forceinline__ void store_hit(const SwParams& p, bool valid, uint32_
 template <int KR, bool SPLIT>
 __device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta& q, int lg, int G,
                                               const uint32_t (&key_a)[KR], const uint32_t (&key_b)[KR],
-                                              uint32_t bias) {
+                                              uint32_t bias, bool f16) {
     uint64_t ga = 0, gb = 0;
 #pragma unroll
     for (int r = 0; r < KR; ++r) {
@@ -298,27 +323,29 @@ __device__ __forceinline__ void finish_coords(const SwParams& p, const PairMeta&
     if constexpr (SPLIT) {
         ga = gb > ga ? gb : ga;
         ga = group_max_u64(ga, lg, G);
-        if (lg == 0) store_hit(p, q.va, q.pa, ga, bias);
+        if (lg == 0) store_hit(p, q.va, q.pa, ga, bias, f16);
     } else {
         ga = group_max_u64(ga, lg, G);
         gb = group_max_u64(gb, lg, G);
         if (lg == 0) {
-            store_hit(p, q.va, q.pa, ga, bias);
-            store_hit(p, q.vb, q.pb, gb, bias);
+            store_hit(p, q.va, q.pa, ga, bias, f16);
+            store_hit(p, q.vb, q.pb, gb, bias, f16);
         }
     }
 }
 
 template <bool SPLIT>
 __device__ __forceinline__ void finish_score(const SwParams& p, const PairMeta& q, int lg, int G,
-                                             uint32_t best, uint32_t bias) {
+                                             uint32_t best, uint32_t bias, bool f16) {
+    // Non-negative f16 bit patterns order like the integers: one u16 max serves both.
     best = group_pk_max(best, lg, G);
     if (lg == 0) {
+        auto val = [&](uint32_t h) { return f16 ? f16_to_score(h) : h - bias; };
         if constexpr (SPLIT) {
-            store_score(p, q.va, q.pa, max(best & 0xFFFFu, best >> 16) - bias);
+            store_score(p, q.va, q.pa, val(max(best & 0xFFFFu, best >> 16)));
         } else {
-            store_score(p, q.va, q.pa, (best & 0xFFFFu) - bias);
-            store_score(p, q.vb, q.pb, (best >> 16) - bias);
+            store_score(p, q.va, q.pa, val(best & 0xFFFFu));
+            store_score(p, q.vb, q.pb, val(best >> 16));
         }
     }
 }
@@ -334,14 +361,23 @@ __device__ __forceinline__ uint32_t from_above(uint32_t own_bottom, uint32_t top
 }
 
 // ---------------------------------------------------------------------------
-// ACGT fast path.  When every window byte of a wave is one of A, C, G, T, the
-// substitution penalty of a packed cell pair is one v_perm_b32 lookup
-// instead of v_xor + v_pk_min: each packed row keeps two 4-byte tables
-// (lo half in bytes 0-3, hi half in bytes 4-7: byte k = 0 if the row's base has
-// class k, else delta), and each window column's LDS word becomes a selector
-// {class(lo), 12, 4 + class(hi), 12} (selector 12 reads 0x00, 13 reads 0xFF:
-// padding columns score a = 0xFF, below every real cell as with the sentinel
-// codes).  The class of A/C/G/T is ((b >> 1) ^ (b >> 2)) & 3 = 0/1/2/3.
+// ACGT fast path.  When every window byte of a wave is one of A, C, G, T (and
+// the scoring scheme fits, p.f16_ok), the DP runs on packed f16 values: a cell
+// of score H holds H * 2^-11, exact for H < 2048, so
+//   * the substitution score s = +match / -mismatch of a packed cell pair is one
+//     v_perm_b32 lookup: both values are f16 numbers whose low byte is zero, so
+//     only their high bytes live in the tables.  Each packed row keeps two
+//     4-byte tables (lo half in bytes 0-3, hi half in bytes 4-7: byte k = hi(+m)
+//     if the row's base has class k, else hi(-mm)), and each window column's
+//     LDS word becomes a selector {12, class(lo), 12, 4 + class(hi)} (selector
+//     12 reads 0x00; padding columns select 0x00 twice, s = +0);
+//   * H_diag + s is one v_pk_add_f16 (negative results are harmless: the
+//     three-way max always sees an E >= 0), and E = max(H - gap, 0) is one
+//     v_pk_add_f16 with the clamp modifier -- two ops fewer per packed row than
+//     the integer path (add match, saturating subtract).
+// The class of A/C/G/T is ((b >> 1) ^ (b >> 2)) & 3 = 0/1/2/3.  Padding
+// columns with s = 0 copy a diagonal value one row down, so a padding cell
+// never beats the real cell it copies (equal score, larger i).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t base_class(uint32_t b) { return ((b >> 1) ^ (b >> 2)) & 3u; }
 
@@ -357,23 +393,26 @@ __device__ __forceinline__ bool code_ok(uint32_t v, uint32_t shift) {
 
 __device__ __forceinline__ uint32_t win_selector(uint32_t word, uint32_t shift) {
     const uint32_t lo = word & 0xFFFFu, hi = word >> 16;
-    const uint32_t sl = (lo & kWinSentinel) ? 13u : base_class(lo >> shift);
-    const uint32_t sh = (hi & kWinSentinel) ? 13u : base_class(hi >> shift);
-    return sl | (12u << 8) | ((4u + sh) << 16) | (12u << 24);
+    const uint32_t sl = (lo & kWinSentinel) ? 12u : base_class(lo >> shift);
+    const uint32_t sh = (hi & kWinSentinel) ? 12u : 4u + base_class(hi >> shift);
+    return 12u | (sl << 8) | (12u << 16) | (sh << 24);
 }
 
 // A read byte outside A/C/G/T (N, lower case, ...) can never equal a window
-// byte of a fast-path wave, so its row (like a padding row) is all delta.
-__device__ __forceinline__ uint32_t row_table(uint32_t v, uint32_t shift, uint32_t d4) {
+// byte of a fast-path wave, so its row (like a padding row) is all mismatch.
+__device__ __forceinline__ uint32_t row_table(uint32_t v, uint32_t shift, uint32_t mis4, uint32_t match_hi) {
     const uint32_t b = v >> shift;
-    return ((v & kReadSentinel) || !is_acgt(b)) ? d4 : d4 & ~(0xFFu << (8u * base_class(b)));
+    if ((v & kReadSentinel) || !is_acgt(b)) return mis4;
+    const uint32_t sh = 8u * base_class(b);
+    return (mis4 & ~(0xFFu << sh)) | (match_hi << sh);
 }
 
 // Checks this lane's share of the group's staged window stream; returns true
 // (wave-uniform) if every window byte of the wave is A/C/G/T, and then
 // rewrites the stream in place as selectors.  Reads may hold any byte.
 __device__ __forceinline__ bool to_fast_path(uint32_t* stream, int words, int lg, int G, bool active,
-                                             uint32_t shift) {
+                                             uint32_t shift, bool allowed) {
+    if (!allowed) return false;
     bool ok = true;
     for (int k = lg; active && k < words; k += G) {
         const uint32_t w = stream[k];
@@ -385,12 +424,94 @@ __device__ __forceinline__ bool to_fast_path(uint32_t* stream, int words, int lg
     return true;
 }
 
+// Fast-path staging straight from the window bytes (16-byte aligned batches):
+// each dword of four columns is classified in SWAR form, checked against
+// A/C/G/T (canonical bytes rebuilt by one v_perm from the classes) and turned
+// into four selector words, written to LDS as 16-byte stores.  Columns past a
+// window get selector 12 (s = 0).  Returns false if this lane saw any other
+// window byte; the caller then stages integer codes instead.
+__device__ __forceinline__ uint32_t class4(uint32_t x) { return ((x >> 1) ^ (x >> 2)) & 0x03030303u; }
+__device__ __forceinline__ uint32_t canon4(uint32_t cl) { return __builtin_amdgcn_perm(0u, 0x54474341u, cl); }
+// 0xFF in each byte e < rem (rem clamped to [0, 4])
+__device__ __forceinline__ uint32_t byte_mask(int rem) {
+    return rem >= 4 ? ~0u : (rem <= 0 ? 0u : ~0u >> (32 - 8 * rem));
+}
+
+// One round of up to kRound 16-column chunks per lane: chunk k = k0 + u * G + lg
+// (two cover 32 G columns: every window up to 384 bp in one round).
+constexpr int kRound = 2;
+struct WinRound {
+    uint4 a[kRound], b[kRound];
+    uint32_t prev[kRound];  // split: the byte before each chunk
+};
+
+template <bool SPLIT>
+__device__ __forceinline__ void load_round(const SwParams& p, uint32_t pa, uint32_t pb, int k0, int lg, int G,
+                                           WinRound& w) {
+    const uint8_t* wa = p.wins + (uint64_t)pa * p.win_stride;
+    const uint8_t* wb = p.wins + (uint64_t)pb * p.win_stride;
+    const int top = (int)(p.win_stride >> 4) - 1;  // last loadable chunk
+    const int last = (int)p.win_stride - 1;
+#pragma unroll
+    for (int u = 0; u < kRound; ++u) {
+        // clamped chunk index: always a legal load; columns past the window are masked
+        const int k = min(k0 + u * G + lg, top);
+        w.a[u] = *reinterpret_cast<const uint4*>(wa + 16 * k);
+        if constexpr (SPLIT) w.prev[u] = wa[min(max(16 * (k0 + u * G + lg) - 1, 0), last)];
+        else w.b[u] = *reinterpret_cast<const uint4*>(wb + 16 * k);
+    }
+}
+
+template <bool SPLIT>
+__device__ __forceinline__ uint32_t sel_round(const PairMeta& q, uint32_t* stream, int k0, int nch, int lg, int G,
+                                              const WinRound& w) {
+    uint32_t bad = 0u;
+#pragma unroll
+    for (int u = 0; u < kRound; ++u) {
+        const int k = k0 + u * G + lg;
+        if (k < nch) {
+            const uint32_t xa[4] = {w.a[u].x, w.a[u].y, w.a[u].z, w.a[u].w};
+            uint32_t xb[4] = {0u, 0u, 0u, 0u};
+            if constexpr (!SPLIT) { xb[0] = w.b[u].x; xb[1] = w.b[u].y; xb[2] = w.b[u].z; xb[3] = w.b[u].w; }
+            uint32_t carry = SPLIT ? (w.prev[u] & 0xFFu) : 0u;
+            uint4* dst = reinterpret_cast<uint4*>(stream + kLead + 16 * k);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int c0 = 16 * k + 4 * d;
+                const uint32_t x_a = xa[d];
+                const uint32_t ma = byte_mask(q.na - c0);
+                uint32_t x_b, mb;
+                if constexpr (SPLIT) {  // high half: column c - 1, valid for 1 <= c <= n
+                    x_b = (x_a << 8) | carry;
+                    carry = x_a >> 24;
+                    mb = byte_mask(q.na + 1 - c0) & (c0 == 0 ? ~0xFFu : ~0u);
+                } else {
+                    x_b = xb[d];
+                    mb = byte_mask(q.nb - c0);
+                }
+                const uint32_t ca = class4(x_a), cb = class4(x_b);
+                bad |= ((canon4(ca) ^ x_a) & ma) | ((canon4(cb) ^ x_b) & mb);
+                const uint32_t sa = (ca & ma) | (0x0C0C0C0Cu & ~ma);
+                const uint32_t sb = ((cb | 0x04040404u) & mb) | (0x0C0C0C0Cu & ~mb);
+                uint32_t o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    // selector bytes {12, sa_e, 12, sb_e}: v_perm leaves 0x00 at bytes 0 and 2
+                    o[e] = __builtin_amdgcn_perm(sb, sa, 0x000C000Cu | (uint32_t)e << 8 | (uint32_t)(4 + e) << 24) |
+                           0x000C000Cu;
+                dst[d] = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+        }
+    }
+    return bad;
+}
+
 // ---------------------------------------------------------------------------
 // The DP.  Per packed cell pair (same (i, j) in both halves):
+//  integer path (any bytes, any scheme):
 //   linear:  a  = min(rc ^ w, delta)            substitution penalty 0 / delta
 //            t1 = sat(DG - a)                   DG = H_diag + match -> max(H_diag + s, 0)
 //            h  = max3(t1, E_left, E_up)        E = sat(H - gap)
-//   (fast path: a = perm(table_hi, table_lo, selector), see above)
 //   affine:  every H, E, F and t1 carries a bias K = 256 + ge (H* = H + K),
 //            which keeps all their subtractions non-negative per u16 half, so
 //            they run as full-rate v_sub_u32/v_add_u32 on the packed pair:
@@ -398,10 +519,16 @@ __device__ __forceinline__ bool to_fast_path(uint32_t* stream, int words, int lg
 //            E*  = max(E*_left - ge, GK_left)     GK = sat(H* - (go+ge+K)) + K
 //            F*  = max(F*_up   - ge, GK_up)       = max(H - go - ge, 0) + K
 //            h*  = max3(t1*, E*, F*)  >= K: the zero floor comes from GK.
-//   DG(next row, next column) = h + match, formed in the row chain (below).
+//  f16 path (ACGT windows, see above), values H * 2^-11:
+//   linear:  t1 = H_diag + s                    s = perm(table_hi, table_lo, selector)
+//            h  = max3(t1, E_left, E_up)        E = clamp(H - gap) >= 0
+//   affine:  G  = clamp(H - go - ge)
+//            E  = max(E_left - ge, G_left),  F = max(F_up - ge, G_up)
+//            h  = max3(t1, E, F)                (E, F >= 0: the zero floor)
+//   Diagonal term of the next row and column, formed in the row chain (below).
 // ---------------------------------------------------------------------------
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
-__device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint32_t* lds) {
+__device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint32_t* lds, uint64_t& t_loop) {
     const int lane = threadIdx.x;
     const int G = (int)p.group_lanes;
     const int g_raw = lane / G;
@@ -419,15 +546,39 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     // wavefront steps, rounded up to even for the two-step unrolled loop
     const int steps = (__builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + skew + 1) & ~1;
     uint32_t* stream = lds + g * p.lds_stride;
-    stage_window<SPLIT>(p, q, stream, steps, lg, G, active);
+    // Staging.  Read bytes and the first round of window chunks are loaded
+    // together (one memory round trip); 16-byte aligned batches under an f16
+    // scheme stage selectors directly and fall back to integer codes only if
+    // some window byte of the wave is not A/C/G/T.
+    uint32_t rb_a[KR], rb_b[KR];
+    load_read_bytes<KR, SPLIT>(p, q.pa, q.pb, lg, rb_a, rb_b);
+    const bool try_fast = p.f16_ok && p.win_vec;
+    WinRound w0;
+    if (try_fast) load_round<SPLIT>(p, q.pa, q.pb, 0, lg, G, w0);
     uint32_t rc[KR];
-    load_read_codes<KR, SPLIT>(p, q, lg, rc);
+    read_codes<KR, SPLIT>(p, q, lg, rb_a, rb_b, rc);
+    bool fast;
+    if (try_fast) {
+        const int nch = (int)((p.lds_stride - kLead) >> 4);  // chunks of the whole stream
+        uint32_t bad = 0u;
+        if (active) {
+            for (int k = lg; k < kLead; k += G) stream[k] = 0x0C0C0C0Cu;
+            bad = sel_round<SPLIT>(q, stream, 0, nch, lg, G, w0);
+            for (int k0 = kRound * G; k0 < nch; k0 += kRound * G) {  // windows past 16 kRound G columns
+                WinRound w;
+                load_round<SPLIT>(p, q.pa, q.pb, k0, lg, G, w);
+                bad |= sel_round<SPLIT>(q, stream, k0, nch, lg, G, w);
+            }
+        }
+        fast = __builtin_amdgcn_ballot_w64(bad != 0u) == 0;
+        if (!fast) stage_window<SPLIT>(p, q, stream, steps, lg, G, active);
+    } else {
+        stage_window<SPLIT>(p, q, stream, steps, lg, G, active);
+        __syncthreads();
+        fast = to_fast_path(stream, kLead + steps, lg, G, active, p.code_shift, p.f16_ok != 0);
+    }
     __syncthreads();
 
-    const uint32_t match2 = p.match2, delta2 = p.delta2, ext2 = p.gap2, oe2 = p.open_ext2;
-    const uint32_t bias2 = AFFINE ? p.bias2 : 0u;           // K in both halves (affine)
-    const uint32_t kmatch2 = add_nc(bias2, match2);
-    const uint32_t og2 = oe2 - bias2;                       // affine: go + ge
     uint32_t E[KR], GK[AFFINE ? KR : 1];
     uint32_t key_a[COORDS ? KR : 1], key_b[COORDS ? KR : 1];
     uint32_t best = 0u;
@@ -436,26 +587,34 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     const uint32_t nj_lane = (uint32_t)(0xFFFF + (SPLIT ? 2 * lg : lg));
     const uint32_t lds_wp = (uint32_t)(uintptr_t)wp;  // LDS byte address of wp[0]
 
-    // The whole DP for one substitution scheme: PERM = ACGT table lookups,
-    // else xor/min on the byte codes.
-    auto run = [&](auto perm_tag) __attribute__((always_inline)) {
-        constexpr bool PERM = decltype(perm_tag)::value;
-        uint32_t tab_lo[PERM ? KR : 1], tab_hi[PERM ? KR : 1];
-        if constexpr (PERM) {
-            const uint32_t d4 = (delta2 & 0xFFu) * 0x01010101u;
+    // The whole DP for one arithmetic domain: F16 = ACGT table lookups on f16
+    // values, else xor/min on the byte codes with u16 integer values.
+    auto run = [&](auto f16_tag) __attribute__((always_inline)) {
+        constexpr bool F16 = decltype(f16_tag)::value;
+        // integer path constants
+        const uint32_t match2 = p.match2, delta2 = p.delta2, ext2 = p.gap2, oe2 = p.open_ext2;
+        const uint32_t bias2 = (AFFINE && !F16) ? p.bias2 : 0u;  // K in both halves (integer affine)
+        const uint32_t kmatch2 = add_nc(bias2, match2);
+        const uint32_t og2 = oe2 - bias2;                       // integer affine: go + ge
+        // f16 path constants: -gap (linear) / -ge (affine), -(go + ge)
+        const uint32_t nge = p.f16_ngap2, noe = p.f16_noe2;
+        uint32_t tab_lo[F16 ? KR : 1], tab_hi[F16 ? KR : 1];
+        if constexpr (F16) {
+            const uint32_t mis4 = (p.f16_hi >> 8) * 0x01010101u, match_hi = p.f16_hi & 0xFFu;
 #pragma unroll
             for (int r = 0; r < KR; ++r) {
-                tab_lo[r] = row_table(rc[r] & 0xFFFFu, p.code_shift, d4);
-                tab_hi[r] = row_table(rc[r] >> 16, p.code_shift, d4);
+                tab_lo[r] = row_table(rc[r] & 0xFFFFu, p.code_shift, mis4, match_hi);
+                tab_hi[r] = row_table(rc[r] >> 16, p.code_shift, mis4, match_hi);
             }
         }
+        // F16: the substitution score s; integer: the penalty a = match - s.
         auto sub = [&](int r, uint32_t w) __attribute__((always_inline)) -> uint32_t {
-            if constexpr (PERM) return __builtin_amdgcn_perm(tab_hi[r], tab_lo[r], w);
+            if constexpr (F16) return __builtin_amdgcn_perm(tab_hi[r], tab_lo[r], w);
             else return pk_min(rc[r] ^ w, delta2);
         };
 #pragma unroll
         for (int r = 0; r < KR; ++r) {
-            E[r] = bias2;                                    // E = 0 (affine: E* = K)
+            E[r] = bias2;                                    // E = 0 (integer affine: E* = K)
             if constexpr (AFFINE) GK[r] = bias2;             // G = 0
             if constexpr (COORDS) { key_a[r] = 0u; key_b[r] = 0u; }
         }
@@ -463,15 +622,15 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
 
         // Software pipeline: t1 (the diagonal term) of step t+1 is formed inside
         // step t's row chain, as soon as the H it needs is known, so each link of
-        // the dependent max3 -> sat-sub chain has independent work beside it
+        // the dependent max3 -> sub chain has independent work beside it
         // (waves issue in order; a lone wave otherwise stalls on every link).
         uint32_t t1a[KR], t1b[KR];
         {
             const uint32_t w0 = wp[0];
 #pragma unroll
             for (int r = 0; r < KR; ++r) {
-                const uint32_t a = sub(r, w0);
-                t1a[r] = AFFINE ? kmatch2 - a : pk_satsub(match2, a);
+                const uint32_t a = sub(r, w0);               // H_diag = 0
+                t1a[r] = F16 ? a : (AFFINE ? kmatch2 - a : pk_satsub(match2, a));
             }
         }
         // One wavefront step: consumes t1 (this step's diagonal terms), produces
@@ -481,13 +640,20 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
                         __attribute__((always_inline)) {
             // Unbiased values cross the lanes (the zero fill is the top boundary),
             // the bias is re-added on arrival: no u16 half ever goes negative.
-            // Only H (and affine F) cross: E resp. GK of the row above are
+            // Only H (and affine F) cross: E resp. G of the row above are
             // functions of its H, recomputed here instead of a second DPP move.
             const uint32_t h_up = from_above<SPLIT>(h_bot - bias2, top_mask);
-            const uint32_t d_up = add_nc(h_up, kmatch2);
-            uint32_t up;    // linear: E of the row above; affine: F* of the row above
-            uint32_t g_up;  // affine: GK of the row above
-            if constexpr (AFFINE) {
+            uint32_t up;    // linear: E of the row above; affine: F of the row above
+            uint32_t g_up;  // affine: G of the row above
+            if constexpr (F16) {
+                if constexpr (AFFINE) {
+                    up = from_above<SPLIT>(f_bot, top_mask);
+                    g_up = hadd_clamp(h_up, noe);
+                } else {
+                    up = hadd_clamp(h_up, nge);
+                    g_up = 0u;
+                }
+            } else if constexpr (AFFINE) {
                 up = add_nc(from_above<SPLIT>(f_bot - bias2, top_mask), bias2);
                 g_up = add_nc(pk_satsub(h_up, og2), bias2);
             } else {
@@ -498,14 +664,27 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
 #pragma unroll
             for (int r = 0; r < KR; ++r) a_n[r] = sub(r, w);
             // row 0's diagonal next step: the lane above's H now
-            t1n[0] = AFFINE ? d_up - a_n[0] : pk_satsub(d_up, a_n[0]);
+            if constexpr (F16) t1n[0] = hadd(h_up, a_n[0]);
+            else t1n[0] = AFFINE ? add_nc(h_up, kmatch2) - a_n[0] : pk_satsub(add_nc(h_up, kmatch2), a_n[0]);
             const uint32_t nj_a = (nj_lane - (uint32_t)t) & 0xFFFFu;
             const uint32_t nj_b = SPLIT ? ((nj_lane + 1u - (uint32_t)t) & 0xFFFFu) : nj_a;
             uint32_t hprev = 0u;
 #pragma unroll
             for (int r = 0; r < KR; ++r) {
                 uint32_t h;
-                if constexpr (AFFINE) {
+                if constexpr (F16) {
+                    if constexpr (AFFINE) {
+                        const uint32_t e = hmax(hadd(E[r], nge), GK[r]);
+                        up = hmax(hadd(up, nge), g_up);
+                        h = pk_max3(t1[r], e, up);
+                        E[r] = e;
+                        g_up = GK[r] = hadd_clamp(h, noe);
+                    } else {
+                        h = pk_max3(t1[r], E[r], up);
+                        up = E[r] = hadd_clamp(h, nge);
+                    }
+                    if (r + 1 < KR) t1n[r + 1] = hadd(h, a_n[r + 1]);
+                } else if constexpr (AFFINE) {
                     const uint32_t e = pk_max(E[r] - ext2, GK[r]);     // full-rate sub, no borrow
                     up = pk_max(up - ext2, g_up);
                     h = pk_max3(t1[r], e, up);
@@ -523,13 +702,13 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
                     key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj_b);
                 } else {
                     if (r & 1) best = track_max3(best, hprev, h);
-                    else if (r + 1 == KR) best = pk_max(best, h);
+                    else if (r + 1 == KR) best = F16 ? hmax(best, h) : pk_max(best, h);
                     hprev = h;
                 }
             }
             if constexpr (AFFINE) f_bot = up;
         };
-        // Step count rounded up to even: the extra step scores sentinel columns,
+        // Step count rounded up to even: the extra step scores padding columns,
         // which never reach a real cell's score.
         // The window words are read from LDS one full iteration (two steps) before
         // use, so a lone wave never waits on LDS latency.  The read is an asm
@@ -549,20 +728,20 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
         }
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
     };
-    // Words of the group's stream the loop consumes (all staged).
-    const int words = kLead + steps;
-    const bool fast = to_fast_path(stream, words, lg, G, active, p.code_shift);
+    if (p.trace) t_loop = __builtin_amdgcn_s_memrealtime();
     if (fast) run(std::true_type{});
     else run(std::false_type{});
 
-    if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, G, key_a, key_b, bias2 & 0xFFFFu);
-    else finish_score<SPLIT>(p, q, lg, G, best, bias2 & 0xFFFFu);
+    const uint32_t bias = fast ? 0u : (p.bias2 & 0xFFFFu) * (AFFINE ? 1u : 0u);
+    if constexpr (COORDS) finish_coords<KR, SPLIT>(p, q, lg, G, key_a, key_b, bias, fast);
+    else finish_score<SPLIT>(p, q, lg, G, best, bias, fast);
     return fast;
 }
 
 // Diagnostics (MSW_WAVE_TRACE, tools/wave_trace.py): per block, start and end
 // on the 100 MHz constant clock, the shader-clock cycles between them, the
-// wave's HW_ID / XCC_ID and what it ran.
+// ticks spent before the DP loop (staging), the wave's HW_ID / XCC_ID and
+// what it ran.
 struct WaveClock {
     uint64_t t0, c0;
 };
@@ -575,7 +754,7 @@ __device__ __forceinline__ WaveClock trace_begin(const SwParams& p) {
     return w;
 }
 __device__ __forceinline__ void trace_end(const SwParams& p, const WaveClock& w, bool fast, bool split,
-                                          int kr) {
+                                          int kr, uint64_t t_loop) {
     if (!p.trace) return;
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
@@ -587,7 +766,8 @@ __device__ __forceinline__ void trace_end(const SwParams& p, const WaveClock& w,
         o[1] = t1;
         o[2] = (uint64_t)hw_id | ((uint64_t)xcc << 32) | ((uint64_t)fast << 40) | ((uint64_t)split << 41) |
                ((uint64_t)kr << 48);
-        o[3] = c1 - w.c0;
+        // shader cycles (40 bits) | constant-clock ticks before the DP loop << 40
+        o[3] = ((c1 - w.c0) & 0xFFFFFFFFFFull) | ((t_loop - w.t0) << 40);
     }
 }
 
@@ -596,8 +776,9 @@ template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
 __global__ __launch_bounds__(64) void sw_kernel(SwParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const WaveClock wc = trace_begin(p);
-    const bool fast = sw_body<KR, AFFINE, COORDS, SPLIT>(p, blockIdx.x, lds);
-    trace_end(p, wc, fast, SPLIT, KR);
+    uint64_t t_loop = 0;
+    const bool fast = sw_body<KR, AFFINE, COORDS, SPLIT>(p, blockIdx.x, lds, t_loop);
+    trace_end(p, wc, fast, SPLIT, KR, t_loop);
 }
 
 // Mixed grid for small batches: blocks [0, p.pairs_blocks) run the pairs
@@ -609,17 +790,19 @@ template <int KRP, bool AFFINE, bool COORDS>
 __global__ __launch_bounds__(64) void sw_mixed_kernel(SwParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const WaveClock wc = trace_begin(p);
+    uint64_t t_loop = 0;
     if (blockIdx.x < p.pairs_blocks) {
-        const bool fast = sw_body<KRP, AFFINE, COORDS, false>(p, blockIdx.x, lds);
-        trace_end(p, wc, fast, false, KRP);
+        const bool fast = sw_body<KRP, AFFINE, COORDS, false>(p, blockIdx.x, lds, t_loop);
+        trace_end(p, wc, fast, false, KRP, t_loop);
     } else {
         SwParams q = p;
         const uint32_t done = p.pairs_blocks * pairs_per_wave(false, p.groups);
         q.n_slots = p.n_slots - done;
         q.order = p.order ? p.order + done : nullptr;
         if (!p.order) q.slot_base = done;
-        const bool fast = sw_body<(KRP + 1) / 2, AFFINE, COORDS, true>(q, blockIdx.x - p.pairs_blocks, lds);
-        trace_end(p, wc, fast, true, (KRP + 1) / 2);
+        const bool fast = sw_body<(KRP + 1) / 2, AFFINE, COORDS, true>(q, blockIdx.x - p.pairs_blocks, lds,
+                                                                      t_loop);
+        trace_end(p, wc, fast, true, (KRP + 1) / 2, t_loop);
     }
 }
 

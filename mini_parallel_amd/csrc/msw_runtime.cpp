@@ -71,6 +71,10 @@ struct Scheme {
     uint32_t match2, delta2, gap2, open_ext2, bias2, code_shift;
     int32_t match;
     uint32_t bias;  // affine value bias K (0 for linear)
+    // f16 fast path: match and mismatch are f16 values with a zero low byte
+    // (the v_perm tables hold high bytes only); per-launch bound in f16_fits.
+    bool f16_scheme;
+    uint32_t f16_hi, f16_ngap2, f16_noe2;
 };
 
 int make_scheme(const msw_scoring_t* sc, Scheme* s) {
@@ -99,7 +103,22 @@ int make_scheme(const msw_scoring_t* sc, Scheme* s) {
     s->bias = s->affine ? 256u + (uint32_t)sc->gap_extend : 0u;
     s->bias2 = dup16(s->bias);
     s->open_ext2 = dup16((uint32_t)(sc->gap_open + sc->gap_extend) + s->bias);
+    // f16 domain (cells H * 2^-11, exact below 2048): gaps of 2048 or more
+    // zero any cell, exactly as 2047 does, so they are capped there.
+    const uint32_t mb = msw::f16_cell_bits(sc->match), xb = msw::f16_cell_bits(sc->mismatch);
+    s->f16_scheme = (mb & 0xFFu) == 0 && (xb & 0xFFu) == 0;
+    s->f16_hi = (mb >> 8) | ((xb >> 8) << 8);
+    const int32_t ge = std::min(sc->gap_extend, 2047);
+    const int32_t oe = std::min(sc->affine ? sc->gap_open + sc->gap_extend : sc->gap_extend, 2047);
+    s->f16_ngap2 = dup16(msw::f16_cell_bits(-ge));
+    s->f16_noe2 = dup16(msw::f16_cell_bits(-oe));
     return MSW_OK;
+}
+
+// The f16 path holds every cell value (<= match * min(m, n)) below 2048.
+bool f16_fits(const Scheme& s, uint32_t max_m, uint32_t max_n) {
+    if (getenv("MSW_NO_F16")) return false;  // tests: force the integer path
+    return s.f16_scheme && (uint64_t)s.match * (std::min(max_m, max_n) + 2u) < 2048u;
 }
 
 // Score bound: every cell value (and H + match) must stay a finite,
@@ -125,6 +144,9 @@ msw::SwParams base_params(const Scheme& s) {
     p.gap2 = s.gap2;
     p.open_ext2 = s.open_ext2;
     p.bias2 = s.bias2;
+    p.f16_hi = s.f16_hi;
+    p.f16_ngap2 = s.f16_ngap2;
+    p.f16_noe2 = s.f16_noe2;
     return p;
 }
 
@@ -268,7 +290,11 @@ static double simd_cycles_per_instr(uint64_t k) {
 
 LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const Scheme& sch, int cu_count) {
     const uint64_t simds = 4ull * (uint64_t)(cu_count > 0 ? cu_count : 256);
-    const double per_row = 5.5 + (sch.affine ? 5.2 : 0.0) + (sch.coords ? 2.8 : 0.0);
+    // VALU instructions per packed row of the compiled loops:
+    // f16 path 4.8 (+4.1 affine, +2.6 coordinates); integer path 5.5 (+5.2, +2.8).
+    const bool f16 = f16_fits(sch, max_m, max_n);
+    const double per_row = f16 ? 4.8 + (sch.affine ? 4.1 : 0.0) + (sch.coords ? 2.6 : 0.0)
+                               : 5.5 + (sch.affine ? 5.2 : 0.0) + (sch.coords ? 2.8 : 0.0);
     auto wave_instr = [&](bool split, uint32_t G) {
         const int kr = msw::rows_per_lane(max_m, split, G);
         const double steps = (double)max_n + (split ? 2.0 * G : (double)G);
@@ -394,6 +420,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.n_slots = b.count;
         p.lds_stride = msw::stream_stride(b.max_n);
         p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+        p.f16_ok = f16_fits(sch, b.max_m, b.max_n) ? 1u : 0u;
         const LaunchPlan plan = choose_layout(b.count, b.max_m, b.max_n, sch, ctx->cu_count);
         p.pairs_blocks = plan.pairs_blocks;
         p.group_lanes = plan.group_lanes;
@@ -666,6 +693,7 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     p.n_slots = (uint32_t)b->n_pairs;
     p.lds_stride = msw::stream_stride(max_win_len);
     p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+    p.f16_ok = f16_fits(sch, max_read_len, max_win_len) ? 1u : 0u;
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
     const LaunchPlan plan = choose_layout(b->n_pairs, max_read_len, max_win_len, sch, ctx->cu_count);
     p.pairs_blocks = plan.pairs_blocks;

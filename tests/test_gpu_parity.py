@@ -107,9 +107,24 @@ def test_config5_mixed_lengths(gpu_ctx, layout, oracle):
         assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
 
 
+@pytest.mark.parametrize("coords", [False, True])
+@pytest.mark.parametrize("affine", [False, True])
+def test_integer_domain_on_acgt(gpu_ctx, layout, oracle, monkeypatch, affine, coords):
+    """MSW_NO_F16 forces the u16 integer path (xor/min substitution) on
+    ACGT windows that would otherwise take the f16 table path."""
+    monkeypatch.setenv("MSW_NO_F16", "1")
+    b = config_batch(2, n_pairs=3000, seed_offset=91)
+    sc = Scoring(gap_open=3 if affine else 0, gap_extend=1 if affine else 2, affine=affine, want_coords=coords)
+    assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), coords)
+
+
 @pytest.mark.parametrize("match,mismatch,go,ge,affine", [
     (1, 0, 0, 1, False), (1, -1, 0, 1, False), (5, -4, 0, 3, False), (3, -2, 0, 0, False),
     (1, -3, 5, 2, True), (2, -1, 3, 1, True), (4, -60, 10, 1, True), (2, 0, 1, 1, True),
+    # f16 fast path off: 9 and -9 are not f16 values with a zero low byte; 16 * 200 >= 2048
+    (9, -9, 0, 2, False), (16, -8, 0, 4, False), (16, -8, 20, 3, True),
+    # gap penalties of 2048 and more (capped in the f16 domain)
+    (2, -1, 0, 1024, False), (2, -1, 5000, 1024, True),
 ])
 def test_scoring_schemes(gpu_ctx, layout, oracle, match, mismatch, go, ge, affine):
     b = make_pairs(3000, (1, 200), 1.7, seed=match * 100 + ge, read_stride=208, win_stride=352)

@@ -40,7 +40,9 @@ def decode(path):
 
 def summarise(blk):
     used = blk[blk[:, 1] != 0]
-    t0, t1, info, cyc = (used[:, i].astype(np.int64) for i in range(4))
+    t0, t1, info, w3 = (used[:, i].astype(np.int64) for i in range(4))
+    cyc = w3 & ((1 << 40) - 1)
+    pro_us = (w3 >> 40) / 100.0  # staging before the DP loop
     hw = info & 0xFFFFFFFF
     xcc = (info >> 32) & 0xFF
     fast = (info >> 40) & 1
@@ -61,6 +63,7 @@ def summarise(blk):
         "eff_clock_ghz": round(float((cyc / np.maximum(t1 - t0, 1) * 100e6).mean() / 1e9), 3),
         "simds_used": int(np.unique(key).size),
         "cus_used": int(np.unique(key // 4).size),
+        "prologue_us": {"p50": round(float(np.median(pro_us)), 2), "max": round(float(pro_us.max()), 2)},
     }
     for sp in (0, 1):
         m = split == sp
