@@ -34,12 +34,15 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 # VALU issue cycles per packed row-step (one wave instruction stream covering
-# 64 lanes x 2 cells = 128 cells): the compiled loop's instruction mix (ACGT
-# fast path, KR = 10, tools/issue_sim.py cost table) priced at the per-op issue
-# costs measured by tools/ubench_valu.hip (packed/max/perm ops 4.1 cycles,
-# add 2.2, DPP 4.4).  The xor/min path costs +2.2.
-CYCLES_PER_ROW_STEP = {"linear": 21.82, "linear_coords": 32.51, "affine": 35.82,
-                       "affine_coords": 46.51}
+# 64 lanes x 2 cells = 128 cells) of the f16 fast path at full occupancy: the
+# compiled loop's VALU instructions per row-step (hipcc -S of msw_kernels.hip,
+# KR = 13: linear 124 / 26, +coords 192 / 26, affine 230 / 26, affine+coords
+# 298 / 26) x 4.1 cycles, the issue cost of v_pk_add_f16, v_pk_maximum3_f16,
+# v_perm_b32, v_lshl_or_b32, v_bfi_b32 and v_max3_u32 measured by
+# tools/ubench_valu.hip.  A lone wave issues at most one
+# instruction per ~4.75 cycles, so one-wave-per-SIMD batches sit below this.
+CYCLES_PER_ROW_STEP = {"linear": 19.55, "linear_coords": 30.28, "affine": 36.27,
+                       "affine_coords": 46.99}
 
 
 def parse():
@@ -221,7 +224,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u16",
+            "dtype": "f16",
+            "dtype_note": "cells are exact integers held as packed f16 (H * 2^-11, H < 2048; "
+                          "DESIGN.md 4.1); the u16 integer path serves non-ACGT windows",
             "data": "synthetic (seeded genome, 1% subs, 0.1% indels, 0.05% N, 10% unrelated reads)",
             "config": {"workload": f"config{cfg}: {batch.n_pairs} pairs/GPU, reads {int(batch.read_len.min())}-"
                                    f"{max_m} bp x windows {int(batch.win_len.min())}-{max_n} bp, "
@@ -236,8 +241,9 @@ def main():
                      "ceiling_gcups": round(valu_ceiling, 1),
                      "frac": round(kernel_gcups / valu_ceiling, 4),
                      "cycles_per_packed_row_step": CYCLES_PER_ROW_STEP[kind],
-                     "basis": "VALU issue bound of the kernel's instruction mix at 2.4 GHz "
-                              "(peak clock; ~2.2 GHz sustained, tools/wave_trace.py; DESIGN.md 4)"},
+                     "basis": "VALU issue bound of the f16 loop's instruction mix at full "
+                              "occupancy, 2.4 GHz peak clock (~2.2 GHz sustained, "
+                              "tools/wave_trace.py; DESIGN.md 4)"},
             "cpu_baseline": cpu,
             "parity": parity,
             "pcie_inclusive": pcie,
