@@ -527,6 +527,27 @@ __device__ __forceinline__ uint32_t sel_round(const PairMeta& q, uint32_t* strea
 //            h  = max3(t1, E, F)                (E, F >= 0: the zero floor)
 //   Diagonal term of the next row and column, formed in the row chain (below).
 // ---------------------------------------------------------------------------
+// Row-group scheduling of the f16 loop (kPermLead in sw_body), per variant:
+// 0 = hipcc's own schedule.  MI355X, 10k pairs (tools/ab_sweep.sh): linear
+// 54.0 -> 49.8 us with 2 (1: 53.1, 3: 53.8); every other variant is as fast
+// or faster with 0 (linear + coords 66.4 vs 67.6, affine + coords 97.0 vs 111).
+#ifndef MSW_PERM_LEAD_LIN
+#define MSW_PERM_LEAD_LIN 2
+#endif
+#ifndef MSW_PERM_LEAD_LIN_COORDS
+#define MSW_PERM_LEAD_LIN_COORDS 0
+#endif
+#ifndef MSW_PERM_LEAD_AFF
+#define MSW_PERM_LEAD_AFF 0
+#endif
+#ifndef MSW_PERM_LEAD_AFF_COORDS
+#define MSW_PERM_LEAD_AFF_COORDS 0
+#endif
+constexpr int perm_lead(bool affine, bool coords) {
+    return affine ? (coords ? MSW_PERM_LEAD_AFF_COORDS : MSW_PERM_LEAD_AFF)
+                  : (coords ? MSW_PERM_LEAD_LIN_COORDS : MSW_PERM_LEAD_LIN);
+}
+
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
 __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint32_t* lds, uint64_t& t_loop) {
     const int lane = threadIdx.x;
@@ -660,9 +681,17 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
                 up = pk_satsub(h_up, ext2);
                 g_up = 0u;
             }
+            // Substitution terms of the next column.  With kPermLead > 0 the f16
+            // loop issues them kPermLead rows ahead, one per row group, and fences
+            // each row group (sched_barrier): a lone wave issues in order, and a
+            // perm between the max3 -> clamp -> max3 links of the row chain fills
+            // the wait for their results (hipcc otherwise bunches the perms up
+            // front).  Measured per variant (perm_lead above).
+            constexpr int kPermLead = F16 ? perm_lead(AFFINE, COORDS) : 0;
             uint32_t a_n[KR];
 #pragma unroll
-            for (int r = 0; r < KR; ++r) a_n[r] = sub(r, w);
+            for (int r = 0; r < KR; ++r)
+                if (!kPermLead || r < kPermLead) a_n[r] = sub(r, w);
             // row 0's diagonal next step: the lane above's H now
             if constexpr (F16) t1n[0] = hadd(h_up, a_n[0]);
             else t1n[0] = AFFINE ? add_nc(h_up, kmatch2) - a_n[0] : pk_satsub(add_nc(h_up, kmatch2), a_n[0]);
@@ -673,6 +702,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
             for (int r = 0; r < KR; ++r) {
                 uint32_t h;
                 if constexpr (F16) {
+                    if (kPermLead && r + kPermLead < KR) a_n[r + kPermLead] = sub(r + kPermLead, w);
                     if constexpr (AFFINE) {
                         const uint32_t e = hmax(hadd(E[r], nge), GK[r]);
                         up = hmax(hadd(up, nge), g_up);
@@ -705,6 +735,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
                     else if (r + 1 == KR) best = F16 ? hmax(best, h) : pk_max(best, h);
                     hprev = h;
                 }
+                if constexpr (kPermLead > 0) __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (AFFINE) f_bot = up;
         };
