@@ -120,6 +120,23 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
                            msw_out_t* out, uint32_t max_read_len, uint32_t max_win_len,
                            void* stream);
 
+/* Length-bucketed plan for a device-resident batch of mixed lengths (BASELINE
+ * config 5).  Built on the host from host copies of the length arrays (the
+ * FASTQ loader has them): pairs are grouped by rows per lane (read length /
+ * 16) and by window length, and the slot -> pair order is uploaded once;
+ * msw_align_batch_planned then scores the whole batch in ONE kernel launch,
+ * heaviest bucket first, enqueued on `stream` like msw_align_batch_device.
+ * A plan belongs to its context and fixes the scoring scheme and the lengths:
+ * reuse it for every pass over the same batch.  This is the device-resident
+ * form of msw_align_batch's per-chunk bucketing (which replaces the
+ * one-string-per-call gpu_align loop, aligner.rs:269-289). */
+typedef struct msw_plan msw_plan;
+int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_len,
+                    const uint16_t* win_len, uint64_t n_pairs, msw_plan** out);
+int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_t* batch,
+                            msw_out_t* out, void* stream);
+void msw_plan_destroy(msw_plan* plan);
+
 /* == gpu_align(seq1, seq2, device) (aligner.rs:410-532): the kernel the
  * reference actually launches (smith_waterman.cl:11-71) with its host geometry
  * W = min(max_wg, 1024) (aligner.rs:422), G = min(ceil(L/W), max_groups)

@@ -26,6 +26,7 @@ EXPORTED = (
     "msw_align_batch", "msw_align_batch_async", "msw_wait", "msw_align_batch_device",
     "msw_align_compat", "msw_host_alloc", "msw_host_free", "msw_dev_alloc", "msw_dev_free",
     "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
+    "msw_plan_create", "msw_align_batch_planned", "msw_plan_destroy",
 )
 # include/msw_fastq.h
 FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_stats",
@@ -83,6 +84,9 @@ def _declare(L):
         "msw_wait": (I, [P, ctypes.c_uint64]),
         "msw_align_batch_device": (I, [P, ctypes.POINTER(ScoringT), ctypes.POINTER(BatchT),
                                        ctypes.POINTER(OutT), ctypes.c_uint32, ctypes.c_uint32, P]),
+        "msw_plan_create": (I, [P, ctypes.POINTER(ScoringT), P, P, ctypes.c_uint64, ctypes.POINTER(P)]),
+        "msw_align_batch_planned": (I, [P, P, ctypes.POINTER(BatchT), ctypes.POINTER(OutT), P]),
+        "msw_plan_destroy": (None, [P]),
         "msw_align_compat": (I, [P, P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.c_uint32,
                                  ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]),
         "msw_host_alloc": (P, [ctypes.c_size_t]),

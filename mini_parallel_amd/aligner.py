@@ -192,6 +192,47 @@ class Context:
                 check(rc)
         return launch
 
+    def prepare_planned_launch(self, reads_ptr: int, read_len_ptr: int, wins_ptr: int,
+                               win_len_ptr: int, read_stride: int, win_stride: int,
+                               read_len, win_len, score_ptr: int, scoring: Scoring = LINEAR,
+                               end_i_ptr: int = 0, end_j_ptr: int = 0, stream: int = 0):
+        """Mixed-length device batch: build the length-bucketed plan once from the
+        host length arrays (msw_plan_create), return a zero-argument callable that
+        enqueues one single-launch pass (msw_align_batch_planned).  The plan is
+        freed with the callable's ``close()``."""
+        rl = np.ascontiguousarray(read_len, dtype=np.uint16)
+        wl = np.ascontiguousarray(win_len, dtype=np.uint16)
+        if rl.shape != wl.shape:
+            raise ValueError("read_len / win_len shapes differ")
+        sc = scoring.to_c()
+        plan = ctypes.c_void_p()
+        check(lib().msw_plan_create(self.handle, ctypes.byref(sc), rl.ctypes.data, wl.ctypes.data,
+                                    rl.size, ctypes.byref(plan)))
+        batch = BatchT(reads_ptr, wins_ptr, read_len_ptr, win_len_ptr, read_stride, win_stride, rl.size)
+        out = OutT(score_ptr, end_i_ptr, end_j_ptr)
+        fn = lib().msw_align_batch_planned
+        args = (self.handle, plan, ctypes.byref(batch), ctypes.byref(out), ctypes.c_void_p(stream or None))
+        keep = (batch, out, sc)
+
+        class _Launch:
+            def __call__(self_inner) -> None:
+                _ = keep
+                rc = fn(*args)
+                if rc:
+                    check(rc)
+
+            def close(self_inner) -> None:
+                if plan.value:
+                    lib().msw_plan_destroy(plan)
+                    plan.value = None
+
+            def __del__(self_inner):
+                try:
+                    self_inner.close()
+                except Exception:
+                    pass
+        return _Launch()
+
     def synchronize(self) -> None:
         check(lib().msw_synchronize(self.handle))
 

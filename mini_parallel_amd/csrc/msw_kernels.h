@@ -93,8 +93,30 @@ inline size_t lds_bytes(uint32_t lds_stride, uint32_t groups) {
 
 enum class Layout { kPairs, kSplit, kMixed };
 
+// Length-bucketed grid (sw_multi_kernel): bucket b holds the slots
+// [slot_begin[b], slot_begin[b] + count[b]) of the order array, all with
+// rows_per_lane(read length) <= kr[b], and owns blocks
+// [b ? block_end[b - 1] : 0, block_end[b]) of ONE launch (pairs layout, G = 16,
+// 8 pairs per block).  Buckets are listed heaviest first, so the long waves
+// are dispatched first and the short ones fill the tail.
+constexpr int kMaxBuckets = 16;
+struct MultiTable {
+    uint32_t n_buckets;
+    uint32_t block_end[kMaxBuckets];
+    uint32_t slot_begin[kMaxBuckets];
+    uint32_t count[kMaxBuckets];
+    uint32_t kr[kMaxBuckets];
+    uint32_t lds_stride[kMaxBuckets];
+    uint32_t f16_ok[kMaxBuckets];
+};
+
 hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, Layout layout,
                      hipStream_t stream);
+
+// All buckets of `t` in one launch; p.order is required (slot -> pair), the
+// per-bucket fields of p (n_slots, lds_stride, f16_ok) come from the table.
+hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, bool coords,
+                           hipStream_t stream);
 
 // smith_waterman_align restated: result must be zeroed before the launch.
 hipError_t launch_compat(const uint8_t* s1, const uint8_t* s2, int32_t* result, uint64_t L,

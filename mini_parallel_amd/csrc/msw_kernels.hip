@@ -837,6 +837,48 @@ __global__ __launch_bounds__(64) void sw_mixed_kernel(SwParams p) {
     }
 }
 
+// Length-bucketed grid (MultiTable): each block finds its bucket (<= 16
+// entries, wave-uniform scalar scan) and runs the pairs layout with that
+// bucket's rows per lane, window stream stride and f16 eligibility.  One
+// launch for a whole mixed-length batch: no per-bucket launch tails.
+template <int KR, bool AFFINE, bool COORDS>
+__device__ __forceinline__ void multi_body(const SwParams& q, uint32_t blk, uint32_t* lds) {
+    const WaveClock wc = trace_begin(q);
+    uint64_t t_loop = 0;
+    const bool fast = sw_body<KR, AFFINE, COORDS, false>(q, blk, lds, t_loop);
+    trace_end(q, wc, fast, false, KR, t_loop);
+}
+
+template <bool AFFINE, bool COORDS>
+__global__ __launch_bounds__(64) void sw_multi_kernel(SwParams p, MultiTable t) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t b = 0;
+    while (b + 1 < t.n_buckets && blockIdx.x >= t.block_end[b]) ++b;
+    const uint32_t blk = blockIdx.x - (b ? t.block_end[b - 1] : 0u);
+    SwParams q = p;
+    q.order = p.order + t.slot_begin[b];
+    q.n_slots = t.count[b];
+    q.lds_stride = t.lds_stride[b];
+    q.f16_ok = t.f16_ok[b];
+    switch (t.kr[b]) {
+        case 1: multi_body<1, AFFINE, COORDS>(q, blk, lds); break;
+        case 2: multi_body<2, AFFINE, COORDS>(q, blk, lds); break;
+        case 3: multi_body<3, AFFINE, COORDS>(q, blk, lds); break;
+        case 4: multi_body<4, AFFINE, COORDS>(q, blk, lds); break;
+        case 5: multi_body<5, AFFINE, COORDS>(q, blk, lds); break;
+        case 6: multi_body<6, AFFINE, COORDS>(q, blk, lds); break;
+        case 7: multi_body<7, AFFINE, COORDS>(q, blk, lds); break;
+        case 8: multi_body<8, AFFINE, COORDS>(q, blk, lds); break;
+        case 9: multi_body<9, AFFINE, COORDS>(q, blk, lds); break;
+        case 10: multi_body<10, AFFINE, COORDS>(q, blk, lds); break;
+        case 11: multi_body<11, AFFINE, COORDS>(q, blk, lds); break;
+        case 12: multi_body<12, AFFINE, COORDS>(q, blk, lds); break;
+        case 13: multi_body<13, AFFINE, COORDS>(q, blk, lds); break;
+        case 14: multi_body<14, AFFINE, COORDS>(q, blk, lds); break;
+        case 15: multi_body<15, AFFINE, COORDS>(q, blk, lds); break;
+        default: multi_body<16, AFFINE, COORDS>(q, blk, lds); break;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // smith_waterman_align (smith_waterman.cl:11-71) restated.  Work item (g, t)
@@ -953,6 +995,28 @@ hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_r
         case 16: return launch_kr<16, false>(p, affine, coords, stream);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, bool coords,
+                           hipStream_t stream) {
+    if (t.n_buckets == 0) return hipSuccess;
+    if (!p.order || t.n_buckets > (uint32_t)kMaxBuckets || p.group_lanes != 16 || p.groups != 4)
+        return hipErrorInvalidValue;
+    uint32_t stride = 0;
+    for (uint32_t b = 0; b < t.n_buckets; ++b) {
+        if (t.kr[b] < 1 || t.kr[b] > 16) return hipErrorInvalidValue;
+        stride = max(stride, t.lds_stride[b]);
+    }
+    const dim3 grid(t.block_end[t.n_buckets - 1]), block(64);
+    const size_t shm = lds_bytes(stride, p.groups);
+    if (affine) {
+        if (coords) hipLaunchKernelGGL((sw_multi_kernel<true, true>), grid, block, shm, stream, p, t);
+        else hipLaunchKernelGGL((sw_multi_kernel<true, false>), grid, block, shm, stream, p, t);
+    } else {
+        if (coords) hipLaunchKernelGGL((sw_multi_kernel<false, true>), grid, block, shm, stream, p, t);
+        else hipLaunchKernelGGL((sw_multi_kernel<false, false>), grid, block, shm, stream, p, t);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_compat(const uint8_t* s1, const uint8_t* s2, int32_t* result, uint64_t L,

@@ -403,8 +403,55 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
     }
 }
 
+// One-launch table of a bucket list (msw::MultiTable): heaviest waves first
+// (rows per lane x window steps), so the tail of the grid is short waves.
+void fill_multi(const std::vector<Bucket>& buckets, const Scheme& sch, msw::MultiTable& t) {
+    std::vector<Bucket> bs(buckets);
+    auto cost = [](const Bucket& b) { return (uint64_t)msw::rows_per_lane(b.max_m, false) * (b.max_n + 16u); };
+    std::stable_sort(bs.begin(), bs.end(), [&](const Bucket& a, const Bucket& b) { return cost(a) > cost(b); });
+    memset(&t, 0, sizeof(t));
+    uint32_t blocks = 0;
+    for (const Bucket& b : bs) {
+        const uint32_t i = t.n_buckets++;
+        blocks += (b.count + msw::kPairsPerWave - 1) / msw::kPairsPerWave;
+        t.block_end[i] = blocks;
+        t.slot_begin[i] = b.begin;
+        t.count[i] = b.count;
+        t.kr[i] = (uint32_t)msw::rows_per_lane(b.max_m, false);
+        t.lds_stride[i] = msw::stream_stride(b.max_n);
+        t.f16_ok[i] = f16_fits(sch, b.max_m, b.max_n) ? 1u : 0u;
+    }
+}
+
+// Several buckets run as one sw_multi_kernel launch, unless MSW_NO_MULTI is
+// set or a layout / group width is forced (MSW_LAYOUT, MSW_GROUP_LANES): then
+// each bucket gets its own launch with that layout (tests cover both).
+bool use_multi(size_t n_buckets) {
+    return n_buckets > 1 && !getenv("MSW_NO_MULTI") && !getenv("MSW_LAYOUT") && !getenv("MSW_GROUP_LANES");
+}
+
 int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const std::vector<Bucket>& buckets,
                    bool use_order, uint32_t read_stride, uint32_t win_stride) {
+    if (use_order && use_multi(buckets.size())) {
+        msw::SwParams p = base_params(sch);
+        p.reads = s.d_reads;
+        p.wins = s.d_wins;
+        p.read_len = s.d_rlen;
+        p.win_len = s.d_wlen;
+        p.order = s.d_order;
+        p.score = s.d_score;
+        p.end_i = sch.coords ? s.d_ei : nullptr;
+        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.read_stride = read_stride;
+        p.win_stride = win_stride;
+        p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+        p.group_lanes = 16;
+        p.groups = 4;
+        msw::MultiTable t;
+        fill_multi(buckets, sch, t);
+        HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
+        return MSW_OK;
+    }
     for (const Bucket& b : buckets) {
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
@@ -703,6 +750,117 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     if (trace_path && *trace_path) return traced_launch(p, sch, max_read_len, plan, st, trace_path);
     HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st));
     return MSW_OK;
+}
+
+}  // extern "C"
+
+struct msw_plan {
+    const msw_ctx* ctx = nullptr;  // identity only: destroy must not touch the context
+    int device = 0;
+    Scheme sch{};
+    uint64_t n = 0;
+    uint32_t max_m = 0, max_n = 0;
+    uint32_t* d_order = nullptr;
+    bool multi = false;
+    msw::MultiTable table{};
+    LaunchPlan single{};
+};
+
+extern "C" {
+
+int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_len, const uint16_t* win_len,
+                    uint64_t n_pairs, msw_plan** out) {
+    if (!ctx || !out) return fail(MSW_E_INVALID, "ctx/out is NULL");
+    *out = nullptr;
+    Scheme sch;
+    int rc;
+    if ((rc = make_scheme(sc, &sch))) return rc;
+    if (n_pairs && (!read_len || !win_len)) return fail(MSW_E_INVALID, "NULL length array");
+    if (n_pairs > 0xFFFFFFFFull) return fail(MSW_E_RANGE, "n_pairs > 2^32-1");
+    uint32_t gm = 0, gn = 0;
+    for (uint64_t i = 0; i < n_pairs; ++i) {
+        gm = std::max<uint32_t>(gm, read_len[i]);
+        gn = std::max<uint32_t>(gn, win_len[i]);
+    }
+    if ((rc = check_bounds(sch, gm, gn))) return rc;
+    if ((rc = set_device(ctx))) return rc;
+    msw_plan* pl = new msw_plan();
+    pl->ctx = ctx;
+    pl->device = ctx->device;
+    pl->sch = sch;
+    pl->n = n_pairs;
+    pl->max_m = gm;
+    pl->max_n = gn;
+    if (n_pairs) {
+        std::vector<uint32_t> order(n_pairs);
+        std::vector<Bucket> buckets;
+        bucket_chunk(read_len, win_len, n_pairs, order.data(), buckets);
+        pl->multi = use_multi(buckets.size());
+        if (pl->multi) fill_multi(buckets, sch, pl->table);
+        else pl->single = choose_layout(n_pairs, gm, gn, sch, ctx->cu_count);
+        rc = grow_dev(&pl->d_order, n_pairs);
+        hipError_t e = rc ? hipSuccess : hipMemcpy(pl->d_order, order.data(), n_pairs * sizeof(uint32_t),
+                                                   hipMemcpyHostToDevice);
+        if (!rc && e != hipSuccess) rc = fail(MSW_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+        if (rc) {
+            msw_plan_destroy(pl);
+            return rc;
+        }
+    }
+    *out = pl;
+    return MSW_OK;
+}
+
+int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_t* b, msw_out_t* out,
+                            void* stream) {
+    if (!ctx || !plan) return fail(MSW_E_INVALID, "ctx/plan is NULL");
+    if (plan->ctx != ctx) return fail(MSW_E_INVALID, "plan belongs to another context");
+    int rc;
+    if ((rc = validate_batch(b, out, plan->sch))) return rc;
+    if (b->n_pairs != plan->n)
+        return fail(MSW_E_INVALID, "batch has %llu pairs, plan %llu", (unsigned long long)b->n_pairs,
+                    (unsigned long long)plan->n);
+    if (plan->n == 0) return MSW_OK;
+    if (plan->max_m > b->read_stride || plan->max_n > b->win_stride)
+        return fail(MSW_E_INVALID, "max length exceeds stride");
+    if ((rc = set_device(ctx))) return rc;
+    const Scheme& sch = plan->sch;
+    msw::SwParams p = base_params(sch);
+    p.reads = b->reads;
+    p.wins = b->wins;
+    p.read_len = b->read_len;
+    p.win_len = b->win_len;
+    p.order = plan->d_order;
+    p.score = out->score;
+    p.end_i = sch.coords ? out->end_i : nullptr;
+    p.end_j = sch.coords ? out->end_j : nullptr;
+    p.read_stride = b->read_stride;
+    p.win_stride = b->win_stride;
+    p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    if (plan->multi) {
+        p.group_lanes = 16;
+        p.groups = 4;
+        HIP_TRY(msw::launch_sw_multi(p, plan->table, sch.affine, sch.coords, st));
+        return MSW_OK;
+    }
+    p.n_slots = (uint32_t)plan->n;
+    p.lds_stride = msw::stream_stride(plan->max_n);
+    p.f16_ok = f16_fits(sch, plan->max_m, plan->max_n) ? 1u : 0u;
+    p.pairs_blocks = plan->single.pairs_blocks;
+    p.group_lanes = plan->single.group_lanes;
+    p.groups = plan->single.groups;
+    HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, plan->max_m, plan->single.layout, st));
+    return MSW_OK;
+}
+
+void msw_plan_destroy(msw_plan* plan) {
+    if (!plan) return;
+    if (plan->d_order) {
+        (void)hipSetDevice(plan->device);
+        (void)hipFree(plan->d_order);
+    }
+    delete plan;
 }
 
 int msw_align_compat(msw_ctx* ctx, const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2, uint32_t wg,

@@ -37,13 +37,20 @@ def assert_same(got, want, coords: bool):
                                f"{list(zip(i[bad[:5]], j[bad[:5]]))} oracle {list(zip(wi[bad[:5]], wj[bad[:5]]))}")
 
 
-@pytest.fixture(params=["pairs", "split", "mixed", "pairs:12", "pairs:9", "pairs:8", "split:11", "split:8"])
+@pytest.fixture(params=["auto", "pairs", "split", "mixed", "pairs:12", "pairs:9", "pairs:8", "split:11",
+                        "split:8"])
 def layout(request, monkeypatch):
     """Every lane-group layout of the kernel, with 16-lane groups and with
     narrower ones (G = 12, 11, 9, 8: idle lanes at the wave's end, groups that
     straddle DPP rows).  The runtime normally picks layout and G per launch
-    from a makespan model; a forced G that cannot hold the batch's reads
+    from a makespan model ("auto"; mixed-length batches then run as one
+    length-bucketed sw_multi_kernel launch); a forced layout launches each
+    length bucket on its own, and a forced G that cannot hold the batch's reads
     (KR > 16, or the LDS budget) falls back to G = 16."""
+    if request.param == "auto":
+        for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
+            monkeypatch.delenv(k, raising=False)
+        return request.param
     lay, _, g = request.param.partition(":")
     monkeypatch.setenv("MSW_LAYOUT", lay)
     if g:
@@ -241,6 +248,75 @@ def test_device_resident_api(gpu_ctx, layout, oracle):
     torch.cuda.synchronize()
     got = (score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy())
     assert_same(got, oracle_run(oracle, b, sc), True)
+
+
+def _device_batch(b):
+    import torch
+    dev = torch.device("cuda", 0)
+    d = {k: torch.from_numpy(np.ascontiguousarray(getattr(b, k))).to(dev) for k in ("reads", "wins")}
+    d["rl"] = torch.from_numpy(np.ascontiguousarray(b.read_len).view(np.int16)).to(dev)
+    d["wl"] = torch.from_numpy(np.ascontiguousarray(b.win_len).view(np.int16)).to(dev)
+    d["score"] = torch.full((b.n_pairs,), -7, dtype=torch.int32, device=dev)
+    d["ei"] = torch.zeros(b.n_pairs, dtype=torch.int16, device=dev)
+    d["ej"] = torch.zeros(b.n_pairs, dtype=torch.int16, device=dev)
+    return d
+
+
+def _planned(gpu_ctx, b, sc, passes=1):
+    import torch
+    d = _device_batch(b)
+    step = gpu_ctx.prepare_planned_launch(d["reads"].data_ptr(), d["rl"].data_ptr(), d["wins"].data_ptr(),
+                                          d["wl"].data_ptr(), b.reads.shape[1], b.wins.shape[1],
+                                          b.read_len, b.win_len, d["score"].data_ptr(), sc,
+                                          d["ei"].data_ptr(), d["ej"].data_ptr(),
+                                          torch.cuda.current_stream().cuda_stream)
+    for _ in range(passes):
+        step()
+    torch.cuda.synchronize()
+    step.close()
+    return d["score"].cpu().numpy(), d["ei"].cpu().numpy(), d["ej"].cpu().numpy()
+
+
+@pytest.mark.parametrize("multi", [True, False])
+@pytest.mark.parametrize("sc", [Scoring(), Scoring(want_coords=True), Scoring(gap_open=3, gap_extend=1, affine=True),
+                                Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)],
+                         ids=["linear", "linear+coords", "affine", "affine+coords"])
+def test_planned_mixed_lengths(gpu_ctx, oracle, monkeypatch, sc, multi):
+    """msw_plan_create + msw_align_batch_planned (config 5 shape, unsorted,
+    device-resident): one length-bucketed launch (multi) or the single-bucket
+    path over the plan's order (MSW_NO_MULTI), twice over the same plan."""
+    for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
+        monkeypatch.delenv(k, raising=False)
+    if not multi:
+        monkeypatch.setenv("MSW_NO_MULTI", "1")
+    b = config_batch(5, n_pairs=9_000, seed_offset=31)
+    assert_same(_planned(gpu_ctx, b, sc, passes=2), oracle_run(oracle, b, sc), sc.want_coords)
+
+
+def test_planned_edge_cases(gpu_ctx, oracle, monkeypatch):
+    """Plans over every read-length bucket at once (1..256 bp, windows 0..600,
+    non-ACGT bytes in some windows so some waves take the integer path),
+    a one-pair plan and an empty plan."""
+    for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
+        monkeypatch.delenv(k, raising=False)
+    rng = np.random.default_rng(5)
+    n = 3000
+    rlen = rng.integers(0, 257, n).astype(np.uint16)
+    wlen = rng.integers(0, 601, n).astype(np.uint16)
+    reads = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=(n, 256)).astype(np.uint8)
+    wins = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=(n, 608)).astype(np.uint8)
+    wins[::7, 5] = ord("N")
+    b = B(reads, rlen, wins, wlen)
+    b.n_pairs = n
+    for sc in (Scoring(want_coords=True), Scoring(gap_open=2, gap_extend=1, affine=True, want_coords=True)):
+        assert_same(_planned(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
+    one = B(reads[:1], rlen[:1], wins[:1], wlen[:1])
+    one.n_pairs = 1
+    assert_same(_planned(gpu_ctx, one, Scoring(want_coords=True)), oracle_run(oracle, one, Scoring()), True)
+    step = gpu_ctx.prepare_planned_launch(0, 0, 0, 0, 16, 16, np.zeros(0, np.uint16), np.zeros(0, np.uint16),
+                                          0, Scoring())
+    step()
+    step.close()
 
 
 def test_compat_kats(gpu_ctx):
