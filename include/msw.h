@@ -102,6 +102,9 @@ void msw_ctx_destroy(msw_ctx* ctx);
 /* Batched scoring from host memory, synchronous.  Streams the batch through
  * pinned staging in chunks of `chunk_pairs` (0 = GPU_CHUNK_SIZE_READS env, or
  * 65536) with H2D copies on the copy stream overlapped with the kernels.
+ * Pageable arrays are staged (rows repacked to 16-byte-rounded strides, so
+ * padding does not cross PCIe); arrays in pinned memory (msw_host_alloc or
+ * hipHostRegister) are copied to the GPU directly.
  * Replaces the per-chunk gpu_align loop of aligner.rs:269-289 / :390-398. */
 int msw_align_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch,
                     msw_out_t* out, uint64_t chunk_pairs);
@@ -150,6 +153,39 @@ int msw_align_compat(msw_ctx* ctx, const uint8_t* s1, size_t n1, const uint8_t* 
  * alloc_host_ptr (aligner.rs:466-475). */
 void* msw_host_alloc(size_t bytes);
 void msw_host_free(void* p);
+
+/* Reference genome resident in HBM.  The --full-wgs sw driver scores each
+ * read against a window of the reference genome; the reference crate builds
+ * every input on the host per chunk (aligner.rs:269-289).  Here the genome is
+ * uploaded once per GPU and windows are cut on the GPU from (position,
+ * length), so a chunk ships reads + 8-byte positions over PCIe instead of
+ * reads + windows (~2.7x fewer bytes at 150 bp x 300 bp).  A genome belongs to
+ * the context it was created on; destroy it before that context. */
+typedef struct msw_genome msw_genome;
+int msw_genome_create(msw_ctx* ctx, const uint8_t* seq, uint64_t len, msw_genome** out);
+void msw_genome_destroy(msw_genome* g);
+uint64_t msw_genome_length(const msw_genome* g);
+
+/* Reads against genome windows: pair p scores reads[p*read_stride ..][0,
+ * read_len[p]) against genome[win_pos[p], win_pos[p] + win_len[p]), the
+ * window clipped at the genome end; win_pos < 0 or >= the genome length is an
+ * empty window (score 0, coordinates (-1,-1)).  Host arrays as in
+ * msw_align_batch (pageable or msw_host_alloc'ed: pinned arrays are copied to
+ * the GPU directly, without staging). */
+typedef struct {
+    const uint8_t* reads;
+    const uint16_t* read_len;
+    uint32_t read_stride;
+    const int64_t* win_pos;
+    const uint16_t* win_len;
+    uint64_t n_pairs;
+} msw_read_batch_t;
+
+int msw_align_reads(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g, const msw_read_batch_t* batch,
+                    msw_out_t* out, uint64_t chunk_pairs);
+/* Same, asynchronous (completes with msw_wait; host arrays must stay alive). */
+int msw_align_reads_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g,
+                          const msw_read_batch_t* batch, msw_out_t* out, uint64_t chunk_pairs, uint64_t* ticket);
 
 /* Device memory helpers for callers that keep batches resident in HBM. */
 void* msw_dev_alloc(msw_ctx* ctx, size_t bytes);

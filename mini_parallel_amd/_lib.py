@@ -27,6 +27,8 @@ EXPORTED = (
     "msw_align_compat", "msw_host_alloc", "msw_host_free", "msw_dev_alloc", "msw_dev_free",
     "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
     "msw_plan_create", "msw_align_batch_planned", "msw_plan_destroy",
+    "msw_genome_create", "msw_genome_destroy", "msw_genome_length", "msw_align_reads",
+    "msw_align_reads_async",
 )
 # include/msw_fastq.h
 FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_stats",
@@ -52,6 +54,12 @@ class BatchT(ctypes.Structure):
                 ("read_len", ctypes.c_void_p), ("win_len", ctypes.c_void_p),
                 ("read_stride", ctypes.c_uint32), ("win_stride", ctypes.c_uint32),
                 ("n_pairs", ctypes.c_uint64)]
+
+
+class ReadBatchT(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_void_p), ("read_len", ctypes.c_void_p),
+                ("read_stride", ctypes.c_uint32), ("win_pos", ctypes.c_void_p),
+                ("win_len", ctypes.c_void_p), ("n_pairs", ctypes.c_uint64)]
 
 
 class OutT(ctypes.Structure):
@@ -87,6 +95,14 @@ def _declare(L):
         "msw_plan_create": (I, [P, ctypes.POINTER(ScoringT), P, P, ctypes.c_uint64, ctypes.POINTER(P)]),
         "msw_align_batch_planned": (I, [P, P, ctypes.POINTER(BatchT), ctypes.POINTER(OutT), P]),
         "msw_plan_destroy": (None, [P]),
+        "msw_genome_create": (I, [P, P, ctypes.c_uint64, ctypes.POINTER(P)]),
+        "msw_genome_destroy": (None, [P]),
+        "msw_genome_length": (ctypes.c_uint64, [P]),
+        "msw_align_reads": (I, [P, ctypes.POINTER(ScoringT), P, ctypes.POINTER(ReadBatchT),
+                                ctypes.POINTER(OutT), ctypes.c_uint64]),
+        "msw_align_reads_async": (I, [P, ctypes.POINTER(ScoringT), P, ctypes.POINTER(ReadBatchT),
+                                      ctypes.POINTER(OutT), ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64)]),
         "msw_align_compat": (I, [P, P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.c_uint32,
                                  ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]),
         "msw_host_alloc": (P, [ctypes.c_size_t]),

@@ -25,7 +25,8 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from ._lib import (MSW_E_INVALID, BatchT, DeviceInfoT, MswError, OutT, ScoringT, check, lib)
+from ._lib import (MSW_E_INVALID, BatchT, DeviceInfoT, MswError, OutT, ReadBatchT, ScoringT, check,
+                   lib)
 
 GPU_WORK_GROUP_SIZE = 1024          # gpu.rs:9
 GPU_MAX_WORK_GROUPS = 1_000_000     # gpu.rs:10
@@ -153,6 +154,36 @@ class Context:
                                     ctypes.byref(out), chunk_pairs))
         return score, ei, ej
 
+    # -- reads against an HBM-resident genome ------------------------------------------
+    def load_genome(self, seq) -> "Genome":
+        """Upload a reference genome (bytes / str / uint8 array) once; windows
+        are then cut on the GPU (msw_genome_create)."""
+        return Genome(self, seq)
+
+    def align_reads(self, genome: "Genome", reads: np.ndarray, read_len: np.ndarray,
+                    win_pos: np.ndarray, win_len: np.ndarray, scoring: Scoring = LINEAR,
+                    chunk_pairs: int = 0):
+        """Score read p against genome[win_pos[p] : win_pos[p] + win_len[p]]
+        (clipped at the genome end; positions outside it score 0).  Returns
+        (score, end_i, end_j) like :meth:`align_batch`."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        read_len = np.ascontiguousarray(read_len, dtype=np.uint16)
+        win_pos = np.ascontiguousarray(win_pos, dtype=np.int64)
+        win_len = np.ascontiguousarray(win_len, dtype=np.uint16)
+        B = reads.shape[0]
+        if read_len.shape[0] != B or win_pos.shape[0] != B or win_len.shape[0] != B:
+            raise MswError(MSW_E_INVALID, "batch arrays disagree on the number of pairs")
+        score = np.zeros(B, np.int32)
+        ei = np.zeros(B, np.int16) if scoring.want_coords else None
+        ej = np.zeros(B, np.int16) if scoring.want_coords else None
+        batch = ReadBatchT(_ptr(reads), _ptr(read_len), reads.shape[1] if reads.ndim == 2 else 0,
+                           _ptr(win_pos), _ptr(win_len), B)
+        out = OutT(_ptr(score), _ptr(ei), _ptr(ej))
+        sc = scoring.to_c()
+        check(lib().msw_align_reads(self.handle, ctypes.byref(sc), genome.handle, ctypes.byref(batch),
+                                    ctypes.byref(out), chunk_pairs))
+        return score, ei, ej
+
     # -- HBM-resident batches ----------------------------------------------------------
     def align_batch_device(self, reads_ptr: int, read_len_ptr: int, wins_ptr: int,
                            win_len_ptr: int, read_stride: int, win_stride: int, n_pairs: int,
@@ -245,6 +276,60 @@ class Context:
         check(lib().msw_align_compat(self.handle, b1, len(s1), b2, len(s2), wg, max_groups,
                                      ctypes.byref(res)))
         return int(res.value)
+
+
+class Genome:
+    """A reference genome resident in HBM on one context (msw_genome_*)."""
+
+    def __init__(self, ctx: Context, seq):
+        if isinstance(seq, str):
+            seq = seq.encode()
+        a = np.ascontiguousarray(np.frombuffer(bytes(seq), np.uint8) if isinstance(seq, (bytes, bytearray))
+                                 else seq, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        check(lib().msw_genome_create(ctx.handle, _ptr(a) if a.size else None, a.size, ctypes.byref(h)))
+        self._h = h
+        self.ctx = ctx  # keeps the context alive for as long as the genome
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise MswError(MSW_E_INVALID, "genome is closed")
+        return self._h
+
+    def __len__(self) -> int:
+        return int(lib().msw_genome_length(self.handle))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            lib().msw_genome_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """A numpy array in page-locked host memory (msw_host_alloc): batches held
+    in such arrays are copied to the GPU directly, without staging.  The
+    memory is freed when the array (and every view of it) is collected."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    p = lib().msw_host_alloc(max(n, 1))
+    if not p:
+        check(-5)
+    buf = (ctypes.c_uint8 * max(n, 1)).from_address(p)
+    arr = np.frombuffer(buf, dtype=np.uint8, count=n).view(dt).reshape(shape)
+
+    class _Owner:
+        def __del__(self_inner):
+            lib().msw_host_free(p)
+    # numpy keeps `buf` alive through arr.base; hang the owner on the ctypes buffer
+    buf._owner = _Owner()
+    return arr
 
 
 _contexts: dict = {}

@@ -463,9 +463,13 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         fflush(stdout);
     };
 
-    // Readers: as many concurrent files as GPUs x 2 (gzip is single-stream).
+    // Readers: one thread per lane file in flight (a gzip stream inflates on
+    // one core; zlib gives ~0.5-0.75 M reads/s per thread, far below what one
+    // GPU scores, so the host side wants every file open at once).  Default
+    // min(files, 16) -- the box's CPU share -- or MSW_READERS.
     std::atomic<size_t> next_file{0};
-    const int nreaders = std::max(1, std::min<int>((int)todo.size(), 2 * ngpu));
+    const int want_readers = atoi(env_or("MSW_READERS", "16").c_str());
+    const int nreaders = std::max(1, std::min<int>((int)todo.size(), std::max(want_readers, 2 * ngpu)));
     std::vector<std::thread> readers;
     std::atomic<int> readers_left{nreaders};
     for (int r = 0; r < nreaders; ++r) {
@@ -517,47 +521,76 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         workers.emplace_back([&, g]() {
             Ctx ctx(devices[g].ordinal);
             const msw_scoring_t sc = scoring_of(a);
-            std::vector<uint8_t> wins;
-            std::vector<uint16_t> wlen;
-            std::vector<int32_t> score;
-            std::vector<int16_t> ei, ej;
+            // sw mode: the reference genome lives in this GPU's HBM; a chunk
+            // ships reads + window positions, windows are cut on the GPU.
+            msw_genome* gen = nullptr;
+            if (sw && msw_genome_create(ctx.h, (const uint8_t*)genome.data(), genome.size(), &gen) != MSW_OK)
+                die(std::string("GPU genome upload error: ") + msw_last_error());
+            // One chunk in flight while the next is staged (msw_align_reads_async
+            // + msw_wait on the previous ticket).
+            struct InFlight {
+                std::unique_ptr<Chunk> c;
+                std::vector<uint16_t> want;
+                std::vector<int32_t> score;
+                std::vector<int16_t> ei, ej;
+                uint64_t ticket = 0;
+                unsigned long long cells = 0, bases = 0;
+                bool failed = false;
+            };
+            auto settle = [&](InFlight& fl) {
+                FileState& f = *st[fl.c->file_index];
+                long long chunk_score = 0;
+                if (!fl.failed && fl.ticket && msw_wait(ctx.h, fl.ticket) != MSW_OK) {
+                    fprintf(stderr, "  GPU %d alignment error: %s\n", g, msw_last_error());
+                    fl.failed = true;
+                }
+                if (fl.failed) {
+                    f.failed = true;
+                } else {
+                    for (uint64_t i = 0; i < fl.c->n; ++i) chunk_score += fl.score[i];
+                    cells += fl.cells;
+                }
+                f.score += chunk_score;
+                f.bases += fl.bases;
+                f.reads += fl.c->n;
+                if (f.outstanding.fetch_sub(1) == 1 && f.reader_done.load()) finish_file(fl.c->file_index);
+                fl.c.reset();
+            };
+            std::unique_ptr<InFlight> prev;
             for (;;) {
                 std::unique_ptr<Chunk> c = queue.pop();
                 if (!c) break;
                 FileState& f = *st[c->file_index];
-                long long chunk_score = 0;
                 unsigned long long nb = 0;
                 for (uint64_t i = 0; i < c->n; ++i) nb += c->rlen[i];
                 if (sw) {
-                    // window = reference[pos : pos + W] (W = --window or 2 x read length)
-                    const uint32_t ws = 512;
-                    wins.assign(c->n * ws, 0);
-                    wlen.assign(c->n, 0);
-                    score.assign(c->n, 0);
-                    ei.assign(c->n, 0);
-                    ej.assign(c->n, 0);
-                    unsigned long long cc = 0;
+                    // window = reference[pos : pos + W] (W = --window or 2 x read
+                    // length, at most the kernel's 4096), clipped at the genome end
+                    std::unique_ptr<InFlight> fl(new InFlight());
+                    fl->bases = nb;
+                    fl->want.resize(c->n);
+                    fl->score.assign(c->n, 0);
+                    fl->ei.assign(c->n, 0);
+                    fl->ej.assign(c->n, 0);
                     for (uint64_t i = 0; i < c->n; ++i) {
+                        const uint32_t w = std::min<uint32_t>(a.window > 0 ? (uint32_t)a.window : 2u * c->rlen[i], 4096u);
+                        fl->want[i] = (uint16_t)w;
                         const int64_t p = c->pos[i];
-                        uint32_t w = a.window > 0 ? (uint32_t)a.window : 2u * c->rlen[i];
-                        w = std::min<uint32_t>(w, ws);
-                        if (p < 0 || (uint64_t)p >= genome.size()) { wlen[i] = 0; continue; }
-                        w = (uint32_t)std::min<uint64_t>(w, genome.size() - (uint64_t)p);
-                        memcpy(wins.data() + i * ws, genome.data() + p, w);
-                        wlen[i] = (uint16_t)w;
-                        cc += (unsigned long long)w * c->rlen[i];
+                        if (p >= 0 && (uint64_t)p < genome.size())
+                            fl->cells += (unsigned long long)std::min<uint64_t>(w, genome.size() - (uint64_t)p) * c->rlen[i];
                     }
-                    msw_batch_t b{c->reads.data(), wins.data(), c->rlen.data(), wlen.data(), kReadStride, ws, c->n};
-                    msw_out_t o{score.data(), ei.data(), ej.data()};
-                    if (msw_align_batch(ctx.h, &sc, &b, &o, 0) != MSW_OK) {
+                    msw_read_batch_t rb{c->reads.data(), c->rlen.data(), kReadStride, c->pos.data(), fl->want.data(), c->n};
+                    msw_out_t o{fl->score.data(), fl->ei.data(), fl->ej.data()};
+                    fl->c = std::move(c);
+                    if (msw_align_reads_async(ctx.h, &sc, gen, &rb, &o, 0, &fl->ticket) != MSW_OK) {
                         fprintf(stderr, "  GPU %d alignment error: %s\n", g, msw_last_error());
-                        f.failed = true;
-                    } else {
-                        for (uint64_t i = 0; i < c->n; ++i) chunk_score += score[i];
-                        cells += cc;
+                        fl->failed = true;
                     }
+                    if (prev) settle(*prev);
+                    prev = std::move(fl);
                 } else {
                     // compat: chunk concat self-aligned (aligner.rs:269-276, :365-373)
+                    long long chunk_score = 0;
                     std::string cat;
                     cat.reserve(nb);
                     for (uint64_t i = 0; i < c->n; ++i) cat.append((const char*)c->reads.data() + i * kReadStride, c->rlen[i]);
@@ -571,12 +604,14 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         }
                         chunk_score = s;
                     }
+                    f.score += chunk_score;
+                    f.bases += nb;
+                    f.reads += c->n;
+                    if (f.outstanding.fetch_sub(1) == 1 && f.reader_done.load()) finish_file(c->file_index);
                 }
-                f.score += chunk_score;
-                f.bases += nb;
-                f.reads += c->n;
-                if (f.outstanding.fetch_sub(1) == 1 && f.reader_done.load()) finish_file(c->file_index);
             }
+            if (prev) settle(*prev);
+            msw_genome_destroy(gen);
         });
     }
     for (auto& t : readers) t.join();

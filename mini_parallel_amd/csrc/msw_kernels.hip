@@ -911,6 +911,41 @@ __global__ __launch_bounds__(256) void sw_compat_kernel(const uint8_t* __restric
     if ((threadIdx.x & 63) == 0 && best > 0) atomicMax(result, best);
 }
 
+// ---------------------------------------------------------------------------
+// Window cut for genome-resident batches (msw_align_reads): pair p's window
+// genome[pos[p], pos[p] + wlen[p]) -> out[p * ws ..], zero-padded to ws.  One
+// thread per 16-byte output chunk: five aligned dword loads, v_alignbyte to
+// the window's byte offset, one 16-byte store (consecutive threads write
+// consecutive chunks of a row).  The host clips wlen to the genome and pads
+// the genome allocation by >= 20 bytes, so the fifth dword never leaves it.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cut_windows_kernel(const uint8_t* __restrict__ g,
+                                                          const int64_t* __restrict__ pos,
+                                                          const uint16_t* __restrict__ wlen,
+                                                          uint8_t* __restrict__ out, uint32_t chunks,
+                                                          uint64_t ws, uint64_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t p = t / chunks;
+    if (p >= n) return;
+    const uint32_t c = (uint32_t)(t - p * chunks);
+    const int rem = (int)wlen[p] - 16 * (int)c;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (rem > 0) {
+        const uint64_t a = (uint64_t)pos[p] + 16u * c;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(g + (a & ~3ull));
+        uint32_t x[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) x[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], (uint32_t)(a & 3u));
+            const int nb = rem - 4 * k;
+            w[k] = nb >= 4 ? v : (nb > 0 ? v & ((1u << (8 * nb)) - 1u) : 0u);
+        }
+    }
+    *reinterpret_cast<uint4*>(out + p * ws + 16ull * c) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 
 // ---------------------------------------------------------------------------
 // Launchers.
@@ -1016,6 +1051,18 @@ hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, 
         if (coords) hipLaunchKernelGGL((sw_multi_kernel<false, true>), grid, block, shm, stream, p, t);
         else hipLaunchKernelGGL((sw_multi_kernel<false, false>), grid, block, shm, stream, p, t);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_cut_windows(const uint8_t* genome, const int64_t* pos, const uint16_t* wlen, uint8_t* out,
+                              uint32_t ws, uint64_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (ws == 0 || ws % 16 != 0 || ((uintptr_t)out & 15) != 0) return hipErrorInvalidValue;
+    const uint32_t chunks = ws / 16;
+    const uint64_t blocks = (n * chunks + 255) / 256;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cut_windows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, genome, pos, wlen, out,
+                       chunks, (uint64_t)ws, n);
     return hipGetLastError();
 }
 

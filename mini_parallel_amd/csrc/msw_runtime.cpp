@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -150,32 +151,52 @@ msw::SwParams base_params(const Scheme& s) {
     return p;
 }
 
-// Device + pinned buffers for one in-flight chunk.
+// Device + pinned buffers for one in-flight chunk.  The per-pair metadata of a
+// chunk (window positions, slot order, read and window lengths) is one block,
+// [pos i64 | order u32 | rlen u16 | wlen u16] x cap_pairs, uploaded by ONE
+// copy; the results [score i32 | end_i i16 | end_j i16] come back by one.
 struct Slot {
     size_t cap_pairs = 0, cap_read = 0, cap_win = 0;
-    uint8_t *d_reads = nullptr, *d_wins = nullptr;
-    uint16_t *d_rlen = nullptr, *d_wlen = nullptr;
-    uint32_t* d_order = nullptr;
-    int32_t* d_score = nullptr;
-    int16_t *d_ei = nullptr, *d_ej = nullptr;
-    uint8_t *h_reads = nullptr, *h_wins = nullptr;
-    uint16_t *h_rlen = nullptr, *h_wlen = nullptr;
-    uint32_t* h_order = nullptr;
-    int32_t* h_score = nullptr;
-    int16_t *h_ei = nullptr, *h_ej = nullptr;
+    uint8_t *d_reads = nullptr, *d_wins = nullptr, *d_meta = nullptr, *d_res = nullptr;
+    uint8_t *h_reads = nullptr, *h_wins = nullptr, *h_meta = nullptr, *h_res = nullptr;
+    // views into d_meta / h_meta and d_res / h_res
+    int64_t *d_pos = nullptr, *h_pos = nullptr;
+    uint32_t *d_order = nullptr, *h_order = nullptr;
+    uint16_t *d_rlen = nullptr, *d_wlen = nullptr, *h_rlen = nullptr, *h_wlen = nullptr;
+    int32_t *d_score = nullptr, *h_score = nullptr;
+    int16_t *d_ei = nullptr, *d_ej = nullptr, *h_ei = nullptr, *h_ej = nullptr;
     hipEvent_t uploaded = nullptr, done = nullptr;
     bool busy = false;
+    uint64_t ticket = 0;  // msw_align_*_async call that owns the chunk in flight
     // Pending readback bookkeeping.
     uint64_t first = 0, count = 0;
     msw_out_t out{};
 };
 
+constexpr size_t kMetaBytesPerPair = 8 + 4 + 2 + 2;
+constexpr size_t kResBytesPerPair = 4 + 2 + 2;
+
+// Views of the metadata / result blocks for a chunk of n pairs (each array
+// packed at n entries, so one copy moves exactly the chunk's bytes).
+void set_views(Slot& s, uint64_t n) {
+    auto views = [n](uint8_t* meta, uint8_t* res, int64_t*& pos, uint32_t*& order, uint16_t*& rlen, uint16_t*& wlen,
+                     int32_t*& score, int16_t*& ei, int16_t*& ej) {
+        pos = reinterpret_cast<int64_t*>(meta);
+        order = reinterpret_cast<uint32_t*>(meta + 8 * n);
+        rlen = reinterpret_cast<uint16_t*>(meta + 12 * n);
+        wlen = reinterpret_cast<uint16_t*>(meta + 14 * n);
+        score = reinterpret_cast<int32_t*>(res);
+        ei = reinterpret_cast<int16_t*>(res + 4 * n);
+        ej = reinterpret_cast<int16_t*>(res + 6 * n);
+    };
+    views(s.d_meta, s.d_res, s.d_pos, s.d_order, s.d_rlen, s.d_wlen, s.d_score, s.d_ei, s.d_ej);
+    views(s.h_meta, s.h_res, s.h_pos, s.h_order, s.h_rlen, s.h_wlen, s.h_score, s.h_ei, s.h_ej);
+}
+
 void free_slot(Slot& s) {
-    for (void* p : {(void*)s.d_reads, (void*)s.d_wins, (void*)s.d_rlen, (void*)s.d_wlen, (void*)s.d_order,
-                    (void*)s.d_score, (void*)s.d_ei, (void*)s.d_ej})
+    for (void* p : {(void*)s.d_reads, (void*)s.d_wins, (void*)s.d_meta, (void*)s.d_res})
         if (p) (void)hipFree(p);
-    for (void* p : {(void*)s.h_reads, (void*)s.h_wins, (void*)s.h_rlen, (void*)s.h_wlen, (void*)s.h_order,
-                    (void*)s.h_score, (void*)s.h_ei, (void*)s.h_ej})
+    for (void* p : {(void*)s.h_reads, (void*)s.h_wins, (void*)s.h_meta, (void*)s.h_res})
         if (p) (void)hipHostFree(p);
     s = Slot{};
 }
@@ -187,12 +208,19 @@ struct msw_ctx {
     int cu_count = 256;
     hipStream_t compute = nullptr, copy = nullptr;
     Slot slots[2];
-    hipEvent_t slot_events[4] = {};
     uint64_t next_ticket = 1, done_ticket = 0;
+    uint64_t slot_seq = 0;  // chunks submitted (slot = slot_seq & 1)
     // compat buffers
     uint8_t *c_s1 = nullptr, *c_s2 = nullptr;
     int32_t* c_res = nullptr;
     size_t c_cap = 0;
+};
+
+struct msw_genome {
+    const msw_ctx* ctx = nullptr;  // identity only
+    int device = 0;
+    uint8_t* d_seq = nullptr;      // len + kGenomePad bytes (cut kernel over-reads <= 20)
+    uint64_t len = 0;
 };
 
 namespace {
@@ -230,12 +258,9 @@ int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     }
     if (pairs > s.cap_pairs) {
-        if ((rc = grow_dev(&s.d_rlen, pairs)) || (rc = grow_dev(&s.d_wlen, pairs)) ||
-            (rc = grow_dev(&s.d_order, pairs)) || (rc = grow_dev(&s.d_score, pairs)) ||
-            (rc = grow_dev(&s.d_ei, pairs)) || (rc = grow_dev(&s.d_ej, pairs)) ||
-            (rc = grow_host(&s.h_rlen, pairs)) || (rc = grow_host(&s.h_wlen, pairs)) ||
-            (rc = grow_host(&s.h_order, pairs)) || (rc = grow_host(&s.h_score, pairs)) ||
-            (rc = grow_host(&s.h_ei, pairs)) || (rc = grow_host(&s.h_ej, pairs)))
+        if ((rc = grow_dev(&s.d_meta, pairs * kMetaBytesPerPair)) ||
+            (rc = grow_host(&s.h_meta, pairs * kMetaBytesPerPair)) ||
+            (rc = grow_dev(&s.d_res, pairs * kResBytesPerPair)) || (rc = grow_host(&s.h_res, pairs * kResBytesPerPair)))
             return rc;
         s.cap_pairs = pairs;
     }
@@ -500,81 +525,230 @@ int validate_batch(const msw_batch_t* b, const msw_out_t* out, const Scheme& sch
     return MSW_OK;
 }
 
-int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* b, msw_out_t* out,
-              uint64_t chunk_pairs, bool sync) {
+// Host-memory batch of either form: pairs (reads + windows) or reads against
+// a genome-resident window source (wins == nullptr, genome + win_pos set).
+struct HostBatch {
+    const uint8_t* reads = nullptr;
+    const uint16_t* read_len = nullptr;
+    uint32_t read_stride = 0;
+    const uint8_t* wins = nullptr;
+    const uint16_t* win_len = nullptr;
+    uint32_t win_stride = 0;
+    const msw_genome* genome = nullptr;
+    const int64_t* win_pos = nullptr;
+    uint64_t n = 0;
+};
+
+// True when [p, p + bytes) lies in page-locked host memory (hipHostMalloc /
+// hipHostRegister): such arrays are DMA'd directly, without staging.
+bool is_pinned(const void* p, size_t bytes) {
+    if (!p || !bytes || getenv("MSW_NO_DIRECT")) return false;
+    for (const void* q : {p, (const void*)((const uint8_t*)p + bytes - 1)}) {
+        hipPointerAttribute_t a;
+        memset(&a, 0, sizeof(a));
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+
+inline uint32_t round16(uint32_t v) { return (v + 15u) & ~15u; }
+
+// Window length actually scored in genome mode: clipped at the genome end,
+// empty for positions outside it.
+inline uint16_t genome_window(int64_t pos, uint16_t want, uint64_t glen) {
+    if (pos < 0 || (uint64_t)pos >= glen) return 0;
+    return (uint16_t)std::min<uint64_t>(want, glen - (uint64_t)pos);
+}
+
+// Copy `n` rows of `len` bytes from stride `src_stride` to `dst_stride`.
+void repack_rows(uint8_t* dst, uint32_t dst_stride, const uint8_t* src, uint32_t src_stride, uint64_t n) {
+    if (dst_stride == src_stride) {
+        memcpy(dst, src, n * src_stride);
+        return;
+    }
+    for (uint64_t i = 0; i < n; ++i) memcpy(dst + i * dst_stride, src + i * src_stride, dst_stride);
+}
+
+// MSW_HOST_TRACE=1: per-call host phase times on stderr (tools / DESIGN.md 5).
+struct HostTrace {
+    bool on = getenv("MSW_HOST_TRACE") != nullptr;
+    double scan = 0, stage = 0, submit = 0, wait = 0;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    double lap() {
+        const auto n = std::chrono::steady_clock::now();
+        const double d = std::chrono::duration<double, std::micro>(n - t).count();
+        t = n;
+        return d;
+    }
+};
+
+int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out_t* out, uint64_t chunk_pairs,
+              bool sync) {
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
     Scheme sch;
     int rc;
     if ((rc = make_scheme(sc, &sch))) return rc;
-    if ((rc = validate_batch(b, out, sch))) return rc;
-    if ((rc = set_device(ctx))) return rc;
-    const uint64_t n = b->n_pairs;
+    if (!out) return fail(MSW_E_INVALID, "out is NULL");
+    const bool gmode = b.genome != nullptr;
+    const uint64_t n = b.n;
     if (n == 0) return MSW_OK;
+    if (!b.reads || !b.read_len || !b.win_len || !out->score || (gmode ? !b.win_pos : !b.wins))
+        return fail(MSW_E_INVALID, "NULL array in batch/out");
+    if (sch.coords && (!out->end_i || !out->end_j))
+        return fail(MSW_E_INVALID, "want_coords set but end_i/end_j is NULL");
+    if (n > 0xFFFFFFFFull) return fail(MSW_E_RANGE, "n_pairs > 2^32-1");
+    if (gmode && (b.genome->ctx != ctx)) return fail(MSW_E_INVALID, "genome belongs to another context");
+    if ((rc = set_device(ctx))) return rc;
+    HostTrace tr;
     // Host-side range checks over the whole batch first: fail before any launch.
     uint32_t gm = 0, gn = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        gm = std::max<uint32_t>(gm, b->read_len[i]);
-        gn = std::max<uint32_t>(gn, b->win_len[i]);
+    for (uint64_t i = 0; i < n; ++i) gm = std::max<uint32_t>(gm, b.read_len[i]);
+    if (gmode) {
+        for (uint64_t i = 0; i < n; ++i)
+            gn = std::max<uint32_t>(gn, genome_window(b.win_pos[i], b.win_len[i], b.genome->len));
+    } else {
+        for (uint64_t i = 0; i < n; ++i) gn = std::max<uint32_t>(gn, b.win_len[i]);
     }
-    if (gm > b->read_stride || gn > b->win_stride)
+    if (gm > b.read_stride || (!gmode && gn > b.win_stride))
         return fail(MSW_E_INVALID, "length exceeds stride (max read %u / stride %u, max window %u / stride %u)",
-                    gm, b->read_stride, gn, b->win_stride);
+                    gm, b.read_stride, gn, b.win_stride);
     if ((rc = check_bounds(sch, gm, gn))) return rc;
 
+    // Direct DMA from pinned caller arrays; otherwise stage through the slot's
+    // pinned buffers with rows repacked to 16-byte-rounded strides.
+    const bool d_reads = is_pinned(b.reads, n * b.read_stride);
+    const bool d_wins = !gmode && is_pinned(b.wins, n * b.win_stride);
+    const uint32_t rs = d_reads ? b.read_stride : std::min(b.read_stride, std::max(16u, round16(gm)));
+    const uint32_t ws = gmode ? std::max(16u, round16(gn))
+                              : (d_wins ? b.win_stride : std::min(b.win_stride, std::max(16u, round16(gn))));
+    if (tr.on) tr.scan += tr.lap();
+
     const uint64_t chunk = chunk_pairs ? chunk_pairs : default_chunk();
+    // Copies go on the copy stream (overlapping the previous chunk's kernels)
+    // unless a synchronous one-chunk call has nothing to overlap with.
+    const bool multi_chunk = n > chunk || !sync;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
     for (uint64_t first = 0; first < n; first += chunk, ++c) {
         const uint64_t cnt = std::min(chunk, n - first);
-        Slot& s = ctx->slots[c & 1];
+        // Slots alternate across calls too, so consecutive async calls overlap.
+        Slot& s = ctx->slots[ctx->slot_seq++ & 1];
+        if (tr.on) tr.submit += tr.lap();
         if ((rc = drain_slot(s))) return rc;  // the slot's previous chunk must be out before reuse
-        if ((rc = ensure_slot(s, cnt, cnt * b->read_stride, cnt * b->win_stride))) return rc;
-        // Stage the chunk in pinned memory.  (FASTQ callers fill these slabs
-        // directly; see msw_fastq.cpp.)
-        memcpy(s.h_reads, b->reads + first * b->read_stride, cnt * b->read_stride);
-        memcpy(s.h_wins, b->wins + first * b->win_stride, cnt * b->win_stride);
-        memcpy(s.h_rlen, b->read_len + first, cnt * sizeof(uint16_t));
-        memcpy(s.h_wlen, b->win_len + first, cnt * sizeof(uint16_t));
+        if (tr.on) tr.wait += tr.lap();
+        if ((rc = ensure_slot(s, cnt, (size_t)cnt * rs, (size_t)cnt * ws))) return rc;
+        set_views(s, cnt);
+        // Bulk rows: DMA'd from the caller's memory when pinned, else staged.
+        const uint8_t* src_reads = b.reads + first * b.read_stride;
+        if (!d_reads) {
+            repack_rows(s.h_reads, rs, src_reads, b.read_stride, cnt);
+            src_reads = s.h_reads;
+        }
+        const uint8_t* src_wins = nullptr;
+        if (!gmode) {
+            src_wins = b.wins + first * b.win_stride;
+            if (!d_wins) {
+                repack_rows(s.h_wins, ws, src_wins, b.win_stride, cnt);
+                src_wins = s.h_wins;
+            }
+        }
+        // Metadata block: lengths (effective window lengths in genome mode),
+        // positions, slot order.
+        memcpy(s.h_rlen, b.read_len + first, cnt * sizeof(uint16_t));
+        if (gmode) {
+            const int64_t* p = b.win_pos + first;
+            const uint16_t* want = b.win_len + first;
+            for (uint64_t i = 0; i < cnt; ++i) s.h_wlen[i] = genome_window(p[i], want[i], b.genome->len);
+            memcpy(s.h_pos, p, cnt * sizeof(int64_t));
+        } else {
+            memcpy(s.h_wlen, b.win_len + first, cnt * sizeof(uint16_t));
+        }
         bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets);
         bool uniform = buckets.size() == 1;
         if (uniform) {
             // One read-length bucket: order only matters if windows vary a lot.
             uint32_t mn = 0xFFFF, mx = 0;
-            for (uint64_t i = 0; i < cnt; ++i) { mn = std::min<uint32_t>(mn, s.h_wlen[i]); mx = std::max<uint32_t>(mx, s.h_wlen[i]); }
+            for (uint64_t i = 0; i < cnt; ++i) {
+                mn = std::min<uint32_t>(mn, s.h_wlen[i]);
+                mx = std::max<uint32_t>(mx, s.h_wlen[i]);
+            }
             uniform = (mx - mn) < 16;
         }
-        // H2D on the copy stream, kernels on the compute stream.
-        HIP_TRY(hipMemcpyAsync(s.d_reads, s.h_reads, cnt * b->read_stride, hipMemcpyHostToDevice, ctx->copy));
-        HIP_TRY(hipMemcpyAsync(s.d_wins, s.h_wins, cnt * b->win_stride, hipMemcpyHostToDevice, ctx->copy));
-        HIP_TRY(hipMemcpyAsync(s.d_rlen, s.h_rlen, cnt * sizeof(uint16_t), hipMemcpyHostToDevice, ctx->copy));
-        HIP_TRY(hipMemcpyAsync(s.d_wlen, s.h_wlen, cnt * sizeof(uint16_t), hipMemcpyHostToDevice, ctx->copy));
-        if (!uniform)
-            HIP_TRY(hipMemcpyAsync(s.d_order, s.h_order, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->copy));
-        HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
-        HIP_TRY(hipStreamWaitEvent(ctx->compute, s.uploaded, 0));
+        if (tr.on) tr.stage += tr.lap();
+        // H2D on the copy stream, kernels on the compute stream (a one-chunk
+        // batch has nothing to overlap: everything goes on the compute stream,
+        // saving the cross-stream event).
+        hipStream_t up = multi_chunk ? ctx->copy : ctx->compute;
+        HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
+        if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
+        // [pos | order | rlen | wlen]: skip the parts this chunk does not use
+        const size_t meta_lo = gmode ? 0 : (uniform ? 12 : 8) * cnt;
+        HIP_TRY(hipMemcpyAsync(s.d_meta + meta_lo, s.h_meta + meta_lo, kMetaBytesPerPair * cnt - meta_lo,
+                               hipMemcpyHostToDevice, up));
+        if (multi_chunk) {
+            HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
+            HIP_TRY(hipStreamWaitEvent(ctx->compute, s.uploaded, 0));
+        }
+        if (gmode)
+            HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, s.d_pos, s.d_wlen, s.d_wins, ws, cnt, ctx->compute));
         if (uniform) {
             buckets.resize(1);
             buckets[0].begin = 0;
         }
-        if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, b->read_stride, b->win_stride))) return rc;
-        HIP_TRY(hipMemcpyAsync(s.h_score, s.d_score, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->compute));
-        if (sch.coords) {
-            HIP_TRY(hipMemcpyAsync(s.h_ei, s.d_ei, cnt * sizeof(int16_t), hipMemcpyDeviceToHost, ctx->compute));
-            HIP_TRY(hipMemcpyAsync(s.h_ej, s.d_ej, cnt * sizeof(int16_t), hipMemcpyDeviceToHost, ctx->compute));
-        }
+        if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws))) return rc;
+        HIP_TRY(hipMemcpyAsync(s.h_res, s.d_res, (sch.coords ? kResBytesPerPair : 4) * cnt, hipMemcpyDeviceToHost,
+                               ctx->compute));
         HIP_TRY(hipEventRecord(s.done, ctx->compute));
         s.busy = true;
+        s.ticket = ctx->next_ticket;  // the ticket an async call returns
         s.first = first;
         s.count = cnt;
         s.out = *out;
         if (!sch.coords) { s.out.end_i = nullptr; s.out.end_j = nullptr; }
     }
     if (sync) {
+        if (tr.on) tr.submit += tr.lap();
         if ((rc = drain_slot(ctx->slots[0])) || (rc = drain_slot(ctx->slots[1]))) return rc;
+        if (tr.on) tr.wait += tr.lap();
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
     }
+    if (tr.on)
+        fprintf(stderr,
+                "[msw host] pairs=%llu chunks=%llu direct(reads=%d wins=%d) rs=%u ws=%u "
+                "scan=%.1fus stage=%.1fus submit=%.1fus wait=%.1fus\n",
+                (unsigned long long)n, (unsigned long long)c, (int)d_reads, (int)d_wins, rs, ws, tr.scan,
+                tr.stage, tr.submit, tr.wait);
     return MSW_OK;
+}
+
+
+HostBatch pairs_batch(const msw_batch_t& b) {
+    HostBatch h;
+    h.reads = b.reads;
+    h.read_len = b.read_len;
+    h.read_stride = b.read_stride;
+    h.wins = b.wins;
+    h.win_len = b.win_len;
+    h.win_stride = b.win_stride;
+    h.n = b.n_pairs;
+    return h;
+}
+
+HostBatch reads_batch(const msw_read_batch_t& b, const msw_genome* g) {
+    HostBatch h;
+    h.reads = b.reads;
+    h.read_len = b.read_len;
+    h.read_stride = b.read_stride;
+    h.win_len = b.win_len;
+    h.genome = g;
+    h.win_pos = b.win_pos;
+    h.n = b.n_pairs;
+    return h;
 }
 
 }  // namespace
@@ -662,13 +836,15 @@ void msw_ctx_destroy(msw_ctx* ctx) {
 
 int msw_align_batch(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch, msw_out_t* out,
                     uint64_t chunk_pairs) {
-    return run_batch(ctx, sc, batch, out, chunk_pairs, true);
+    if (!batch) return fail(MSW_E_INVALID, "batch is NULL");
+    return run_batch(ctx, sc, pairs_batch(*batch), out, chunk_pairs, true);
 }
 
 int msw_align_batch_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* batch, msw_out_t* out,
                           uint64_t chunk_pairs, uint64_t* ticket) {
     if (!ticket) return fail(MSW_E_INVALID, "ticket is NULL");
-    int rc = run_batch(ctx, sc, batch, out, chunk_pairs, false);
+    if (!batch) return fail(MSW_E_INVALID, "batch is NULL");
+    int rc = run_batch(ctx, sc, pairs_batch(*batch), out, chunk_pairs, false);
     if (rc) return rc;
     *ticket = ctx->next_ticket++;
     return MSW_OK;
@@ -679,9 +855,11 @@ int msw_wait(msw_ctx* ctx, uint64_t ticket) {
     if (ticket == 0 || ticket >= ctx->next_ticket) return fail(MSW_E_INVALID, "unknown ticket %llu", (unsigned long long)ticket);
     int rc = set_device(ctx);
     if (rc) return rc;
-    // Tickets complete in order: draining both slots completes every earlier ticket.
-    if ((rc = drain_slot(ctx->slots[0])) || (rc = drain_slot(ctx->slots[1]))) return rc;
-    ctx->done_ticket = ctx->next_ticket - 1;
+    // Drain the chunks of this ticket and of every earlier one (tickets are
+    // enqueued in order on the same streams); later calls stay in flight.
+    for (Slot& s : ctx->slots)
+        if (s.busy && s.ticket <= ticket && (rc = drain_slot(s))) return rc;
+    ctx->done_ticket = std::max(ctx->done_ticket, ticket);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
     return MSW_OK;
@@ -894,6 +1072,59 @@ int msw_align_compat(msw_ctx* ctx, const uint8_t* s1, size_t n1, const uint8_t* 
     HIP_TRY(msw::launch_compat(ctx->c_s1, ctx->c_s2, ctx->c_res, L, W, G, ctx->compute));
     HIP_TRY(hipMemcpyAsync(score, ctx->c_res, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->compute));
     HIP_TRY(hipStreamSynchronize(ctx->compute));
+    return MSW_OK;
+}
+
+int msw_genome_create(msw_ctx* ctx, const uint8_t* seq, uint64_t len, msw_genome** out) {
+    if (!ctx || !out) return fail(MSW_E_INVALID, "ctx/out is NULL");
+    *out = nullptr;
+    if (len && !seq) return fail(MSW_E_INVALID, "seq is NULL");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    msw_genome* g = new msw_genome();
+    g->ctx = ctx;
+    g->device = ctx->device;
+    g->len = len;
+    hipError_t e = hipMalloc((void**)&g->d_seq, len + msw::kGenomePad);
+    if (e != hipSuccess) {
+        delete g;
+        return fail(MSW_E_NOMEM, "hipMalloc(%llu B) for the genome: %s", (unsigned long long)len, hipGetErrorString(e));
+    }
+    e = hipMemsetAsync(g->d_seq + len, 0, msw::kGenomePad, ctx->copy);
+    if (e == hipSuccess && len) e = hipMemcpyAsync(g->d_seq, seq, len, hipMemcpyHostToDevice, ctx->copy);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->copy);
+    if (e != hipSuccess) {
+        msw_genome_destroy(g);
+        return fail(MSW_E_DEVICE, "genome upload: %s", hipGetErrorString(e));
+    }
+    *out = g;
+    return MSW_OK;
+}
+
+void msw_genome_destroy(msw_genome* g) {
+    if (!g) return;
+    if (g->d_seq) {
+        (void)hipSetDevice(g->device);
+        (void)hipFree(g->d_seq);
+    }
+    delete g;
+}
+
+uint64_t msw_genome_length(const msw_genome* g) { return g ? g->len : 0; }
+
+int msw_align_reads(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g, const msw_read_batch_t* batch,
+                    msw_out_t* out, uint64_t chunk_pairs) {
+    if (!batch || !g) return fail(MSW_E_INVALID, "batch/genome is NULL");
+    return run_batch(ctx, sc, reads_batch(*batch, g), out, chunk_pairs, true);
+}
+
+int msw_align_reads_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g,
+                          const msw_read_batch_t* batch, msw_out_t* out, uint64_t chunk_pairs, uint64_t* ticket) {
+    if (!ticket) return fail(MSW_E_INVALID, "ticket is NULL");
+    if (!batch || !g) return fail(MSW_E_INVALID, "batch/genome is NULL");
+    int rc = run_batch(ctx, sc, reads_batch(*batch, g), out, chunk_pairs, false);
+    if (rc) return rc;
+    *ticket = ctx->next_ticket++;
     return MSW_OK;
 }
 

@@ -111,16 +111,43 @@ def config_batch(k: int, n_pairs: int = 0, seed_offset: int = 0) -> PairBatch:
     raise ValueError(f"unknown config {k}")
 
 
+def _write_lane_file(job):
+    """One lane file of write_wgs_dataset (a process-pool job)."""
+    import gzip
+    (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep) = job
+    genome_bases = int(g.shape[0])
+    b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_arr=g,
+                   read_stride=(read_len + 16 + 15) // 16 * 16)
+    # every read gets a window of this genome: unrelated reads (pos -1) are
+    # paired with a random window
+    rng = np.random.default_rng([seed, k])
+    span = genome_bases - int(b.win_len.max())
+    pos = np.where(b.pos >= 0, np.minimum(b.pos, span), rng.integers(0, span, b.n_pairs))
+    rl = b.read_len.astype(np.int64)
+    qual = b"I" * int(rl.max() if b.n_pairs else 0)
+    tag = sample.encode()
+    recs = [b"@%s:%d:%d pos=%d\n%s\n+\n%s\n" % (tag, lane, i, int(pos[i]), b.reads[i, :rl[i]].tobytes(),
+                                                  qual[:rl[i]]) for i in range(b.n_pairs)]
+    with gzip.open(name, "wb", compresslevel=compresslevel) as f:
+        f.write(b"".join(recs))
+    if not keep:
+        return None
+    cols = np.arange(b.wins.shape[1])
+    wins = g[np.minimum(pos[:, None] + cols[None, :], genome_bases - 1)]
+    wins[cols[None, :] >= b.win_len[:, None].astype(np.int64)] = 0
+    return PairBatch(b.reads, b.read_len.copy(), wins, b.win_len.copy(), pos)
+
+
 def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_per_lane: int = 2,
                       reads_per_file: int = 1000, read_len: int = 150, win_factor: float = 2.0,
                       seed: int = 1004, genome_bases: int = 1 << 20, keep_batches: bool = True,
-                      compresslevel: int = 1) -> dict:
+                      compresslevel: int = 1, workers: int = 1) -> dict:
     """Config-4-shaped dataset: lane files {sample}_L{lane:03}_R{r}_001.fastq.gz
     (aligner.rs:198-204 naming) whose headers carry "pos=<window start>", and
     the reference genome as reference.fa.  Returns paths and (keep_batches) the
     pair batches (reads, windows) so tests can score them with the oracle.
-    Vectorised: a million-read lane file takes seconds, not minutes."""
-    import gzip
+    Vectorised, and ``workers`` > 1 writes the lane files in parallel processes
+    (same files either way)."""
     import os
     os.makedirs(out_dir, exist_ok=True)
     rng = np.random.default_rng(seed)
@@ -129,30 +156,21 @@ def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_p
         f.write(">synthetic seed=%d\n" % seed)
         s = g.tobytes().decode()
         f.write("\n".join(s[k:k + 80] for k in range(0, len(s), 80)) + "\n")
-    files, batches = [], []
+    jobs, files = [], []
     k = 0
     for lane in range(1, lanes + 1):
         for r in range(1, reads_per_lane + 1):
-            b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_arr=g,
-                           read_stride=(read_len + 16 + 15) // 16 * 16)
-            # every read gets a window of this genome: unrelated reads (pos -1)
-            # are paired with a random window
-            span = genome_bases - int(b.win_len.max())
-            pos = np.where(b.pos >= 0, np.minimum(b.pos, span), rng.integers(0, span, b.n_pairs))
-            cols = np.arange(b.wins.shape[1])
-            wins = g[np.minimum(pos[:, None] + cols[None, :], genome_bases - 1)]
-            wins[cols[None, :] >= b.win_len[:, None].astype(np.int64)] = 0
             name = os.path.join(out_dir, "%s_L%03d_R%d_001.fastq.gz" % (sample, lane, r))
-            rl = b.read_len.astype(np.int64)
-            qual = b"I" * int(rl.max() if b.n_pairs else 0)
-            tag = sample.encode()
-            recs = [b"@%s:%d:%d pos=%d\n%s\n+\n%s\n" % (tag, lane, i, int(pos[i]), b.reads[i, :rl[i]].tobytes(),
-                                                          qual[:rl[i]]) for i in range(b.n_pairs)]
-            with gzip.open(name, "wb", compresslevel=compresslevel) as f:
-                f.write(b"".join(recs))
+            jobs.append((g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel,
+                         keep_batches))
             files.append(name)
-            if keep_batches:
-                batches.append(PairBatch(b.reads, b.read_len.copy(), wins, b.win_len.copy(), pos))
             k += 1
+    if workers > 1 and len(jobs) > 1:
+        from multiprocessing import get_context
+        with get_context("fork").Pool(min(workers, len(jobs))) as pool:
+            res = pool.map(_write_lane_file, jobs)
+    else:
+        res = [_write_lane_file(j) for j in jobs]
+    batches = [b for b in res if b is not None] if keep_batches else []
     return {"files": files, "reference": os.path.join(out_dir, "reference.fa"), "batches": batches,
             "sample": sample, "lanes": lanes, "reads_per_lane": reads_per_lane}

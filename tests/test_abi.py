@@ -58,6 +58,7 @@ def test_struct_layout():
     assert ctypes.sizeof(_lib.ScoringT) == 24
     assert ctypes.sizeof(_lib.BatchT) == 48
     assert ctypes.sizeof(_lib.OutT) == 24
+    assert ctypes.sizeof(_lib.ReadBatchT) == 48
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present")

@@ -1,0 +1,199 @@
+"""GPU parity of the host-batch data paths that feed the same kernels:
+
+* reads against an HBM-resident genome (msw_genome_create + msw_align_reads):
+  windows cut on the GPU from (position, length), clipped at the genome end;
+* pinned caller arrays (msw_host_alloc) DMA'd directly, without staging;
+* pageable arrays staged with rows repacked to 16-byte-rounded strides.
+
+Every result is compared bit-exactly with the oracle run on windows cut on
+the host with the same semantics.  Run with -m gpu."""
+import os
+
+import numpy as np
+import pytest
+
+import mini_parallel_amd as mpa
+from mini_parallel_amd import Scoring
+from mini_parallel_amd.aligner import pinned_empty
+from mini_parallel_amd.synthetic import make_pairs
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 1)
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+SCHEMES = [Scoring(), Scoring(want_coords=True),
+           Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)]
+
+
+def oracle_run(oracle, reads, read_len, wins, win_len, sc):
+    return oracle.sw_batch(reads, read_len, wins, win_len, match=sc.match, mismatch=sc.mismatch,
+                           gap_open=sc.gap_open, gap_extend=sc.gap_extend, affine=sc.affine,
+                           threads=THREADS)
+
+
+def host_windows(genome: np.ndarray, pos: np.ndarray, want: np.ndarray):
+    """The documented window semantics (msw.h msw_read_batch_t), on the host."""
+    glen = genome.size
+    eff = np.where((pos < 0) | (pos >= glen), 0, np.minimum(want.astype(np.int64), glen - pos))
+    ws = max(16, (int(eff.max()) + 15) // 16 * 16 if eff.size else 16)
+    W = np.zeros((pos.size, ws), np.uint8)
+    for k in range(pos.size):
+        if eff[k]:
+            W[k, :eff[k]] = genome[pos[k]:pos[k] + eff[k]]
+    return W, eff.astype(np.uint16)
+
+
+def assert_same(got, want, coords):
+    s, i, j = got
+    ws, wi, wj = want
+    bad = np.nonzero(s != ws)[0]
+    assert bad.size == 0, f"{bad.size} score mismatches at {bad[:5]}: gpu {s[bad[:5]]} oracle {ws[bad[:5]]}"
+    if coords:
+        bad = np.nonzero((i != wi) | (j != wj))[0]
+        assert bad.size == 0, f"{bad.size} coordinate mismatches at {bad[:5]}"
+
+
+def genome_case(n_pairs, glen, seed, read_stride=160):
+    """Reads sampled from a genome (with substitutions), positions around the
+    read (window = 2 x read length, centred), plus edge positions: negative,
+    past the end, the last base, windows running off the end, zero lengths."""
+    rng = np.random.default_rng(seed)
+    g = rng.choice(ACGT, glen)
+    rl = rng.integers(1, min(256, read_stride) + 1, n_pairs).astype(np.uint16)
+    rl[: n_pairs // 2] = np.minimum(150, read_stride)
+    want = np.minimum(2 * rl.astype(np.int64), 4096).astype(np.uint16)
+    pos = rng.integers(0, glen, n_pairs).astype(np.int64)
+    R = np.zeros((n_pairs, read_stride), np.uint8)
+    for k in range(n_pairs):
+        m = int(rl[k])
+        src = int(min(max(pos[k] + (int(want[k]) - m) // 2, 0), max(glen - m, 0)))
+        r = g[src:src + m].copy()
+        if r.size < m:
+            r = np.concatenate([r, rng.choice(ACGT, m - r.size)])
+        sub = rng.random(m) < 0.02
+        r[sub] = rng.choice(ACGT, int(sub.sum()))
+        R[k, :m] = r
+    edge = [-5, -1, glen, glen + 100, glen - 1, glen - 7, glen - 150, 0]
+    for k, p in enumerate(edge):
+        if k < n_pairs:
+            pos[k] = p
+    if n_pairs > 10:
+        want[9] = 0
+        want[10] = 1
+    return g, R, rl, pos, want
+
+
+@pytest.mark.parametrize("sc", SCHEMES, ids=["linear", "linear_coords", "affine_coords"])
+@pytest.mark.parametrize("chunk", [0, 777])
+def test_genome_windows_match_host_cut(gpu_ctx, oracle, sc, chunk):
+    g, R, rl, pos, want = genome_case(6000, 1_000_003, seed=5)
+    genome = gpu_ctx.load_genome(g)
+    assert len(genome) == g.size
+    got = gpu_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk)
+    W, wl = host_windows(g, pos, want)
+    assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), sc.want_coords)
+    assert got[0][0] == 0 and got[0][2] == 0  # negative / past-the-end positions
+    genome.close()
+
+
+def test_genome_tiny_and_unaligned(gpu_ctx, oracle):
+    """Genomes of 1..37 bases (lengths not a multiple of 4: the cut kernel's
+    dword over-read must stay in the padded allocation), every start position,
+    window lengths up to past the end, odd read stride (byte path)."""
+    rng = np.random.default_rng(11)
+    sc = Scoring(want_coords=True)
+    for glen in (1, 2, 3, 5, 16, 17, 37):
+        g = rng.choice(ACGT, glen)
+        genome = gpu_ctx.load_genome(g.tobytes())
+        pos = np.repeat(np.arange(-1, glen + 1, dtype=np.int64), 3)
+        want = np.tile(np.array([1, glen, glen + 9], np.uint16), glen + 2)
+        n = pos.size
+        R = np.zeros((n, 21), np.uint8)
+        rl = rng.integers(0, 22, n).astype(np.uint16)
+        for k in range(n):
+            R[k, :rl[k]] = rng.choice(ACGT, int(rl[k]))
+        got = gpu_ctx.align_reads(genome, R, rl, pos, want, sc)
+        W, wl = host_windows(g, pos, want)
+        assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), True)
+        genome.close()
+
+
+def test_genome_mixed_lengths_bucketed(gpu_ctx, oracle):
+    """Config 5 shape through the genome path (length-bucketed launch)."""
+    g, R, rl, pos, want = genome_case(8000, 2_000_000, seed=21, read_stride=256)
+    rl[:] = np.random.default_rng(3).integers(75, 251, rl.size)
+    want[:] = 2 * rl
+    genome = gpu_ctx.load_genome(g)
+    for sc in SCHEMES[1:]:
+        got = gpu_ctx.align_reads(genome, R, rl, pos, want, sc)
+        W, wl = host_windows(g, pos, want)
+        assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), True)
+
+
+def test_genome_errors(gpu_ctx):
+    g = gpu_ctx.load_genome(b"ACGT" * 10)
+    R = np.zeros((2, 16), np.uint8)
+    with pytest.raises(mpa.MswError):  # read longer than its stride
+        gpu_ctx.align_reads(g, R, np.array([20, 1], np.uint16), np.zeros(2, np.int64),
+                            np.array([4, 4], np.uint16))
+    other = mpa.Context(0)
+    with pytest.raises(mpa.MswError, match="another context"):
+        other.align_reads(g, R, np.array([4, 1], np.uint16), np.zeros(2, np.int64),
+                          np.array([4, 4], np.uint16))
+    other.close()
+    s, _, _ = gpu_ctx.align_reads(g, R[:0], np.zeros(0, np.uint16), np.zeros(0, np.int64),
+                                  np.zeros(0, np.uint16))
+    assert s.size == 0
+
+
+@pytest.mark.parametrize("sc", SCHEMES[1:], ids=["linear_coords", "affine_coords"])
+def test_pinned_direct_and_staged_agree(gpu_ctx, oracle, monkeypatch, sc):
+    """Pinned arrays are DMA'd from the caller's memory; pageable ones are
+    staged; MSW_NO_DIRECT forces staging of pinned arrays.  All bit-exact."""
+    b = make_pairs(9000, 150, 2.0, seed=77, read_stride=160, win_stride=304)
+    want = oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc)
+    pr = pinned_empty(b.reads.shape, np.uint8)
+    pw = pinned_empty(b.wins.shape, np.uint8)
+    prl = pinned_empty(b.read_len.shape, np.uint16)
+    pwl = pinned_empty(b.win_len.shape, np.uint16)
+    pr[:], pw[:], prl[:], pwl[:] = b.reads, b.wins, b.read_len, b.win_len
+    for direct in (True, False):
+        if direct:
+            monkeypatch.delenv("MSW_NO_DIRECT", raising=False)
+        else:
+            monkeypatch.setenv("MSW_NO_DIRECT", "1")
+        for chunk in (0, 2500):
+            assert_same(gpu_ctx.align_batch(pr, prl, pw, pwl, sc, chunk_pairs=chunk), want, True)
+    monkeypatch.delenv("MSW_NO_DIRECT", raising=False)
+    assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc), want, True)
+
+
+def test_wide_strides_repacked(gpu_ctx, oracle):
+    """Pageable batches with padded strides (256 / 600) are repacked to
+    16-byte-rounded rows during staging; odd strides take the byte-load
+    staging path in the kernel: same results."""
+    base = make_pairs(5000, (60, 150), 2.0, seed=99, read_stride=160, win_stride=304)
+    sc = Scoring(want_coords=True)
+    want = oracle_run(oracle, base.reads, base.read_len, base.wins, base.win_len, sc)
+    rm, wm = int(base.read_len.max()), int(base.win_len.max())
+    for rs, ws in ((256, 600), (rm | 1, wm | 1), (rm, wm), (160, 304)):
+        R = np.zeros((base.n_pairs, rs), np.uint8)
+        W = np.zeros((base.n_pairs, ws), np.uint8)
+        R[:, :rm] = base.reads[:, :rm]
+        W[:, :wm] = base.wins[:, :wm]
+        assert_same(gpu_ctx.align_batch(R, base.read_len, W, base.win_len, sc, chunk_pairs=1999), want, True)
+
+
+def test_pinned_genome_reads(gpu_ctx, oracle):
+    """Genome path with pinned reads / positions (direct DMA)."""
+    g, R, rl, pos, want = genome_case(4000, 500_009, seed=41)
+    genome = gpu_ctx.load_genome(g)
+    pR = pinned_empty(R.shape, np.uint8)
+    prl = pinned_empty(rl.shape, np.uint16)
+    ppos = pinned_empty(pos.shape, np.int64)
+    pwant = pinned_empty(want.shape, np.uint16)
+    pR[:], prl[:], ppos[:], pwant[:] = R, rl, pos, want
+    sc = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)
+    got = gpu_ctx.align_reads(genome, pR, prl, ppos, pwant, sc, chunk_pairs=1500)
+    W, wl = host_windows(g, pos, want)
+    assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), True)

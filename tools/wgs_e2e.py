@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""End-to-end --full-wgs measurement (BASELINE config 4 shape, scaled to one
+box): writes a synthetic lane dataset (8 lanes x 2 reads-files of 150 bp
+FASTQ.gz reads tagged with their reference window, 64 Mbp genome), then runs
+the C++ CLI `rustseq_mini --full-wgs --gpu --score-mode sw` over it: FASTQ.gz
+inflate + parse into read slabs (reader threads) -> genome-resident windows
+cut on the GPU -> batched SW -> per-file i64 score sums.  One JSON line per
+run (the CLI's record + reader count) goes to --out.
+
+  python tools/wgs_e2e.py --reads-per-file 1000000 --readers 4,16 --out gpurun_out/wgs_e2e.jsonl
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dir", default="/tmp/msw_wgs")
+    ap.add_argument("--lanes", type=int, default=8)
+    ap.add_argument("--reads-per-lane", type=int, default=2)
+    ap.add_argument("--reads-per-file", type=int, default=1_000_000)
+    ap.add_argument("--genome-bases", type=int, default=64 << 20)
+    ap.add_argument("--readers", default="16")
+    ap.add_argument("--chunk", type=int, default=65536)
+    ap.add_argument("--workers", type=int, default=16)
+    ap.add_argument("--out", default="gpurun_out/wgs_e2e.jsonl")
+    ap.add_argument("--extra-env", default="", help="K=V,K=V added to the CLI's environment")
+    args = ap.parse_args()
+
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    t0 = time.time()
+    ds = write_wgs_dataset(args.dir, lanes=args.lanes, reads_per_lane=args.reads_per_lane,
+                           reads_per_file=args.reads_per_file, genome_bases=args.genome_bases,
+                           keep_batches=False, workers=args.workers)
+    gen_s = time.time() - t0
+    gz_bytes = sum(os.path.getsize(f) for f in ds["files"])
+    print(f"dataset: {len(ds['files'])} files, {gz_bytes / 1e6:.0f} MB gz, written in {gen_s:.1f} s", flush=True)
+    cli = os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini")
+    os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+    for readers in [int(x) for x in args.readers.split(",")]:
+        rec = os.path.join(args.dir, f"rec_{readers}.json")
+        env = dict(os.environ, WGS_DATA_DIR=args.dir, WGS_SAMPLE_ID="SYN", WGS_LANES=str(args.lanes),
+                   WGS_READS_PER_LANE=str(args.reads_per_lane), GPU_CHUNK_SIZE_READS=str(args.chunk),
+                   WGS_RUN_ID=f"e2e_{readers}_{int(time.time())}", MSW_READERS=str(readers))
+        for kv in filter(None, args.extra_env.split(",")):
+            k, v = kv.split("=", 1)
+            env[k] = v
+        ts = time.time()
+        r = subprocess.run([cli, "--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"],
+                            "--window", "300", "--checkpoint-dir", args.dir, "--json", rec],
+                           env=env, capture_output=True, text=True, timeout=900)
+        wall = time.time() - ts
+        if r.returncode != 0:
+            print(r.stdout[-3000:], r.stderr[-3000:])
+            raise SystemExit(f"CLI failed with {r.returncode}")
+        d = json.load(open(rec))
+        d.update({"readers": readers, "process_wall_s": round(wall, 3), "gz_bytes": gz_bytes,
+                  "chunk_reads": args.chunk, "extra_env": args.extra_env,
+                  "dataset": f"{args.lanes} lanes x {args.reads_per_lane} files x {args.reads_per_file} "
+                             f"150 bp reads, {args.genome_bases} bp genome, window 300"})
+        print(json.dumps(d), flush=True)
+        with open(args.out, "a") as f:
+            f.write(json.dumps(d) + "\n")
+
+
+if __name__ == "__main__":
+    main()
