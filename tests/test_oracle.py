@@ -112,3 +112,16 @@ def test_threads_do_not_change_results(oracle):
     many = oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=7)
     for x, y in zip(one, many):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/smith_waterman/src/smith_waterman.cl"),
+                    reason="reference sources absent (the GPU box uses the prebuilt oracle/_ref)")
+def test_reference_kernel_object_built():
+    """`make -C oracle ref` compiles the reference's own OpenCL kernels for
+    gfx950 (the checker tests/test_gpu_reference_kernel.py runs on the box)."""
+    import subprocess
+    from oracle import ref_cl
+    subprocess.run(["make", "-C", os.path.dirname(ref_cl.__file__), "-s", "ref"], check=True)
+    assert ref_cl.available()
+    data = open(ref_cl.CO, "rb").read()
+    assert data[:4] == b"\x7fELF" and b"smith_waterman_align" in data and b"smith_waterman_detailed" in data
