@@ -73,6 +73,58 @@ def load_pmc_traffic(key: str):
         return None
 
 
+def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j):
+    """The CPU baseline, timed on this host: the inter-sequence SIMD
+    restatement of the oracle (oracle/sw_simd.c, AVX-512BW 32 x int16 lanes /
+    AVX2 16, bit-exact with the scalar oracle by tests/test_oracle.py) over a
+    bounded sample of the timed pairs sized to ~cpu_seconds, plus the scalar
+    oracle on one core for scale.  Parity: GPU vs the SIMD results on the whole
+    sample and vs the scalar oracle on its smaller sample."""
+    from oracle import oracle_lib
+    oracle_lib.build()
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    kw = dict(match=scoring.match, mismatch=scoring.mismatch, gap_open=scoring.gap_open,
+              gap_extend=scoring.gap_extend, affine=scoring.affine)
+    coords = scoring.want_coords
+
+    def cells_of(n):
+        return int((batch.read_len[:n].astype(np.int64) * batch.win_len[:n]).sum())
+
+    # calibrate on a small sample, then size the sample to ~cpu_seconds
+    n0 = min(batch.n_pairs, 256 * threads)
+    ts = time.perf_counter()
+    oracle_lib.sw_batch_simd(batch.reads[:n0], batch.read_len[:n0], batch.wins[:n0], batch.win_len[:n0],
+                             threads=threads, coords=coords, **kw)
+    rate = n0 / max(time.perf_counter() - ts, 1e-6)
+    ns = int(min(batch.n_pairs, max(n0, rate * args.cpu_seconds)))
+    passes = max(1, int(rate * args.cpu_seconds / ns))
+    ts = time.perf_counter()
+    for _ in range(passes):
+        cs, ci, cj, isa = oracle_lib.sw_batch_simd(batch.reads[:ns], batch.read_len[:ns], batch.wins[:ns],
+                                                   batch.win_len[:ns], threads=threads, coords=coords, **kw)
+    dt = time.perf_counter() - ts
+    scells = passes * cells_of(ns)
+    # scalar oracle, one core, ~1/5 of the budget
+    n1 = max(1, min(ns, int(args.cpu_seconds * 0.2 * 2e8 / max(cells_of(1), 1))))
+    ts = time.perf_counter()
+    ss, si, sj = oracle_lib.sw_batch(batch.reads[:n1], batch.read_len[:n1], batch.wins[:n1],
+                                     batch.win_len[:n1], threads=1, **kw)
+    scalar_gcups = cells_of(n1) / max(time.perf_counter() - ts, 1e-9) / 1e9
+    cpu = {"value": round(scells / dt / 1e9, 3), "unit": "GCUPS", "cores": threads, "kind": "port",
+           "sample": f"{passes} pass(es) over the first {ns} of the {batch.n_pairs} timed pairs "
+                     f"({scells} cells, {dt:.1f} s): oracle/sw_simd.c, inter-sequence "
+                     f"{'AVX-512BW 32' if isa == 512 else ('AVX2 16' if isa == 256 else 'scalar 1')} "
+                     f"x int16 lanes, {threads} threads",
+           "cpu_model": oracle_lib.cpu_model(), "isa_bits": isa,
+           "scalar_oracle_1core_gcups": round(scalar_gcups, 4)}
+    mism = int((cs != gpu_scores[:ns]).sum()) + int((ss != gpu_scores[:n1]).sum())
+    if coords:
+        mism += int(((ci != gpu_i[:ns]) | (cj != gpu_j[:ns])).sum())
+        mism += int(((si != gpu_i[:n1]) | (sj != gpu_j[:n1])).sum())
+    parity = {"checked_pairs": ns, "checked_pairs_scalar": n1, "mismatches": mism, "bit_exact": mism == 0}
+    return cpu, parity
+
+
 def pcie_rates(ctx, batch, scoring, cells, gpu_scores):
     from mini_parallel_amd.aligner import pinned_empty
 
@@ -218,34 +270,7 @@ def main():
         cpu = None
         parity = None
         if args.cpu_seconds > 0:
-            from oracle import oracle_lib
-            oracle_lib.build()
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            kw = dict(match=scoring.match, mismatch=scoring.mismatch, gap_open=scoring.gap_open,
-                      gap_extend=scoring.gap_extend, affine=scoring.affine, threads=threads)
-            # calibrate on a small sample, then size the sample to ~cpu_seconds
-            n0 = min(batch.n_pairs, 64 * threads)
-            ts = time.perf_counter()
-            oracle_lib.sw_batch(batch.reads[:n0], batch.read_len[:n0], batch.wins[:n0],
-                                batch.win_len[:n0], **kw)
-            rate = n0 / max(time.perf_counter() - ts, 1e-6)
-            ns = int(min(batch.n_pairs, max(n0, rate * args.cpu_seconds)))
-            passes = max(1, int(rate * args.cpu_seconds / ns))   # repeat to ~cpu_seconds of work
-            ts = time.perf_counter()
-            for _ in range(passes):
-                cs, ci, cj = oracle_lib.sw_batch(batch.reads[:ns], batch.read_len[:ns],
-                                                 batch.wins[:ns], batch.win_len[:ns], **kw)
-            dt = time.perf_counter() - ts
-            scells = passes * int((batch.read_len[:ns].astype(np.int64) * batch.win_len[:ns]).sum())
-            cpu = {"value": round(scells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads,
-                   "kind": "port",
-                   "sample": f"{passes} pass(es) over the first {ns} of the {batch.n_pairs} timed "
-                             f"pairs ({scells} cells, {dt:.1f} s), oracle/sw_oracle.c scalar C, "
-                             f"{threads} threads"}
-            mism = int((cs != gpu_scores[:ns]).sum())
-            if scoring.want_coords:
-                mism += int(((ci != gpu_i[:ns]) | (cj != gpu_j[:ns])).sum())
-            parity = {"checked_pairs": ns, "mismatches": mism, "bit_exact": mism == 0}
+            cpu, parity = cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j)
 
         # PCIe-inclusive rates (never `value`): the same batch from host memory,
         # scores back on the host, best of 3 calls per variant:

@@ -165,3 +165,74 @@ int32_t oracle_compat_align(const uint8_t* s1, size_t n1, const uint8_t* s2, siz
     }
     return result;
 }
+
+/* ---- inter-sequence SIMD baseline (sw_simd.c, compiled per ISA) ---- */
+typedef void (*simd_range_fn)(const uint8_t*, const uint8_t*, const uint16_t*, const uint16_t*, uint32_t, uint32_t,
+                              uint64_t, uint64_t, uint64_t, int, int, int, int, int, int32_t*, int16_t*, int16_t*);
+void oracle_simd_range_avx512(const uint8_t*, const uint8_t*, const uint16_t*, const uint16_t*, uint32_t, uint32_t,
+                              uint64_t, uint64_t, uint64_t, int, int, int, int, int, int32_t*, int16_t*, int16_t*);
+void oracle_simd_range_avx2(const uint8_t*, const uint8_t*, const uint16_t*, const uint16_t*, uint32_t, uint32_t,
+                            uint64_t, uint64_t, uint64_t, int, int, int, int, int, int32_t*, int16_t*, int16_t*);
+
+typedef struct {
+    simd_range_fn fn;
+    batch_job_t jb;
+    uint64_t n_pairs;
+} simd_job_t;
+
+static void* simd_worker(void* arg) {
+    simd_job_t* s = (simd_job_t*)arg;
+    batch_job_t* jb = &s->jb;
+    if (jb->begin < jb->end)
+        s->fn(jb->reads, jb->wins, jb->read_len, jb->win_len, jb->read_stride, jb->win_stride, jb->begin, jb->end,
+              s->n_pairs, jb->match, jb->mismatch, jb->gap_open, jb->gap_extend, jb->affine, jb->score, jb->end_i,
+              jb->end_j);
+    return NULL;
+}
+
+int oracle_simd_isa(void) {
+    __builtin_cpu_init();
+    if (__builtin_cpu_supports("avx512bw")) return 512;
+    if (__builtin_cpu_supports("avx2")) return 256;
+    return 0;
+}
+
+int oracle_sw_batch_simd(const uint8_t* reads, const uint8_t* wins, const uint16_t* read_len,
+                         const uint16_t* win_len, uint32_t read_stride, uint32_t win_stride, uint64_t n_pairs,
+                         int match, int mismatch, int gap_open, int gap_extend, int affine, int32_t* score,
+                         int16_t* end_i, int16_t* end_j, int threads) {
+    const int isa = oracle_simd_isa();
+    if (isa == 0) {
+        oracle_sw_batch(reads, wins, read_len, win_len, read_stride, win_stride, n_pairs, match, mismatch, gap_open,
+                        gap_extend, affine, score, end_i, end_j, threads);
+        return 0;
+    }
+    const uint64_t vw = isa == 512 ? 32 : 16;
+    const uint64_t groups = (n_pairs + vw - 1) / vw;
+    if (threads < 1) threads = 1;
+    if ((uint64_t)threads > groups) threads = groups ? (int)groups : 1;
+    simd_job_t* jobs = (simd_job_t*)calloc((size_t)threads, sizeof(simd_job_t));
+    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    for (int t = 0; t < threads; ++t) {
+        simd_job_t* s = &jobs[t];
+        s->fn = isa == 512 ? oracle_simd_range_avx512 : oracle_simd_range_avx2;
+        s->n_pairs = n_pairs;
+        batch_job_t* jb = &s->jb;
+        jb->reads = reads; jb->wins = wins; jb->read_len = read_len; jb->win_len = win_len;
+        jb->read_stride = read_stride; jb->win_stride = win_stride;
+        jb->begin = groups * (uint64_t)t / (uint64_t)threads * vw;
+        jb->end = groups * (uint64_t)(t + 1) / (uint64_t)threads * vw;
+        jb->match = match; jb->mismatch = mismatch;
+        jb->gap_open = gap_open; jb->gap_extend = gap_extend; jb->affine = affine;
+        jb->score = score; jb->end_i = end_i; jb->end_j = end_j;
+    }
+    if (threads == 1) {
+        simd_worker(&jobs[0]);
+    } else {
+        for (int t = 0; t < threads; ++t) pthread_create(&tids[t], NULL, simd_worker, &jobs[t]);
+        for (int t = 0; t < threads; ++t) pthread_join(tids[t], NULL);
+    }
+    free(jobs);
+    free(tids);
+    return isa;
+}

@@ -57,6 +57,16 @@ void oracle_sw_batch(const uint8_t* reads, const uint8_t* wins,
                      int match, int mismatch, int gap_open, int gap_extend, int affine,
                      int32_t* score, int16_t* end_i, int16_t* end_j, int threads);
 
+/* Same results as oracle_sw_batch (bit-exact), computed by the inter-sequence
+ * SIMD restatement (sw_simd.c: AVX-512BW 32 x int16 lanes, else AVX2 16, else
+ * the scalar code).  Returns the vector width used in bits (512 / 256 / 0).
+ * bench.py times it as the CPU baseline. */
+int oracle_sw_batch_simd(const uint8_t* reads, const uint8_t* wins, const uint16_t* read_len,
+                         const uint16_t* win_len, uint32_t read_stride, uint32_t win_stride, uint64_t n_pairs,
+                         int match, int mismatch, int gap_open, int gap_extend, int affine, int32_t* score,
+                         int16_t* end_i, int16_t* end_j, int threads);
+int oracle_simd_isa(void);
+
 /* Restatement of the kernel the reference launches, smith_waterman_align
  * (smith_waterman.cl:11-71), with the host geometry of gpu_align
  * (aligner.rs:413-424): L = min(n1,n2); W = work-group size; G = min(ceil(L/W), 1e6);

@@ -125,3 +125,21 @@ def test_reference_kernel_object_built():
     assert ref_cl.available()
     data = open(ref_cl.CO, "rb").read()
     assert data[:4] == b"\x7fELF" and b"smith_waterman_align" in data and b"smith_waterman_detailed" in data
+
+
+@pytest.mark.parametrize("affine", [False, True])
+@pytest.mark.parametrize("coords", [False, True])
+def test_simd_baseline_bit_exact(oracle, affine, coords):
+    """The SIMD CPU baseline (bench.py cpu_baseline) equals the scalar oracle:
+    mixed lengths incl. empty pairs, a ragged last group, several schemes."""
+    from mini_parallel_amd.synthetic import make_pairs
+    b = make_pairs(1000 + 13, (0, 200), 1.7, seed=404 + affine, read_stride=208, win_stride=352)
+    for match, mis, go, ge in ((2, -1, 3 if affine else 0, 1 if affine else 2), (5, -4, 10, 3), (1, 0, 0, 1),
+                               (64, 0, 30000, 1024), (3, -61, 7, 0)):
+        want = oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, match=match, mismatch=mis, gap_open=go,
+                               gap_extend=ge, affine=affine, threads=4)
+        s, i, j, isa = oracle.sw_batch_simd(b.reads, b.read_len, b.wins, b.win_len, match=match, mismatch=mis,
+                                            gap_open=go, gap_extend=ge, affine=affine, threads=3, coords=coords)
+        assert np.array_equal(s, want[0]), (match, mis, go, ge, isa)
+        if coords:
+            assert np.array_equal(i, want[1]) and np.array_equal(j, want[2])
