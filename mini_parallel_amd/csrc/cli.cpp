@@ -34,6 +34,7 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <ctime>
 #include <vector>
 
 #include "msw.h"
@@ -412,6 +413,7 @@ struct WgsReport {
     std::vector<FileCheckpoint> results;
     double wall_ms = 0;
     unsigned long long cells = 0;
+    int readers = 0;
 };
 
 WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const std::vector<std::string>& files,
@@ -620,6 +622,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     WgsReport rep;
     rep.wall_ms = ms_since(t_all);
     rep.cells = cells.load();
+    rep.readers = nreaders;
     for (size_t i = 0; i < files.size(); ++i)
         if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
     return rep;
@@ -691,14 +694,39 @@ int main(int argc, char** argv) {
         printf("Wall time: %.2f s", rep.wall_ms / 1000.0);
         if (rep.cells) printf(", %.1f GCUPS end-to-end", rep.cells / (rep.wall_ms * 1e6));
         printf("\n");
+        // Run record: the reference's BenchmarkResult fields (tools/benchmark.rs:17-34;
+        // its fake gpu_utilization_avg / gpu_memory_used_mb are dropped) plus GCUPS.
+        const int ng = std::max(1, std::min<int>(a.num_gpus, (int)devices.size()));
+        const double secs = std::max(rep.wall_ms / 1000.0, 1e-9);
+        char ts[64];
+        {
+            const time_t now = time(nullptr);
+            struct tm tmv;
+            gmtime_r(&now, &tmv);
+            strftime(ts, sizeof(ts), "%Y-%m-%dT%H:%M:%SZ", &tmv);
+        }
+        double ram_gb = 0;
+        {
+            std::ifstream mi("/proc/meminfo");
+            std::string k;
+            double v = 0;
+            if (mi >> k >> v && k == "MemTotal:") ram_gb = v / (1024.0 * 1024.0);
+        }
+        const double gcups = rep.cells ? rep.cells / (rep.wall_ms * 1e6) : 0.0;
         std::ostringstream j;
-        j << "{\"mode\": \"full_wgs\", \"score_mode\": \"" << a.score_mode << "\", \"run_id\": \"" << ck.run_id
-          << "\", \"num_gpus\": " << std::max(1, std::min<int>(a.num_gpus, (int)devices.size()))
+        j << "{\"timestamp\": \"" << ts << "\", \"run_id\": \"" << ck.run_id << "\", \"mode\": \"full_wgs\""
+          << ", \"score_mode\": \"" << a.score_mode << "\", \"files_processed\": " << rep.results.size()
           << ", \"total_files\": " << files.size() << ", \"total_reads\": " << reads << ", \"total_bases\": " << bases
-          << ", \"total_score\": " << total << ", \"wall_ms\": " << rep.wall_ms << ", \"cells\": " << rep.cells
-          << ", \"gcups_end_to_end\": " << (rep.cells ? rep.cells / (rep.wall_ms * 1e6) : 0.0)
-          << ", \"reads_per_second\": " << (reads / std::max(rep.wall_ms / 1000.0, 1e-9))
-          << ", \"host_cores\": " << std::thread::hardware_concurrency() << "}\n";
+          << ", \"total_score\": " << total << ", \"total_time_seconds\": " << secs << ", \"wall_ms\": " << rep.wall_ms
+          << ", \"throughput_reads_per_second\": " << reads / secs
+          << ", \"throughput_bases_per_second\": " << bases / secs << ", \"chunk_size\": " << get_chunk_size_reads()
+          << ", \"cpu_cores_used\": " << rep.readers << ", \"parallel_files\": " << (rep.readers > 1 ? "true" : "false")
+          << ", \"system_info\": {\"gpu_name\": \"" << json_escape(devices.empty() ? "" : devices[0].name)
+          << "\", \"gpu_memory_gb\": " << (devices.empty() ? 0.0 : devices[0].memory_gb)
+          << ", \"cpu_cores\": " << std::thread::hardware_concurrency() << ", \"total_ram_gb\": " << ram_gb << "}"
+          << ", \"num_gpus\": " << ng << ", \"host_cores\": " << std::thread::hardware_concurrency()
+          << ", \"cells\": " << rep.cells << ", \"gcups\": " << gcups << ", \"gcups_end_to_end\": " << gcups
+          << ", \"reads_per_second\": " << reads / secs << "}\n";
         write_json(a.json, j.str());
         return all_ok ? 0 : 1;
     }

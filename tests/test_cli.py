@@ -115,6 +115,13 @@ def test_full_wgs_sw_and_resume(tmp_path, oracle):
         want += per_file[-1]
     rec = json.load(open(tmp_path / "rec.json"))
     assert rec["total_score"] == want and rec["total_reads"] == 6000
+    # the reference's BenchmarkResult fields (tools/benchmark.rs:17-34) + GCUPS
+    for k in ("timestamp", "run_id", "mode", "files_processed", "total_reads", "total_bases", "total_score",
+              "total_time_seconds", "throughput_reads_per_second", "throughput_bases_per_second", "chunk_size",
+              "cpu_cores_used", "parallel_files", "system_info", "gcups", "num_gpus", "host_cores"):
+        assert k in rec, k
+    assert rec["files_processed"] == 4 and rec["chunk_size"] == 700 and rec["gcups"] > 0
+    assert set(rec["system_info"]) == {"gpu_name", "gpu_memory_gb", "cpu_cores", "total_ram_gb"}
     ck = json.load(open(tmp_path / "checkpoint_t1.json"))
     assert ck["completed_files"] == 4
     assert [f["score"] for f in sorted(ck["files"], key=lambda f: f["file_index"])] == per_file
