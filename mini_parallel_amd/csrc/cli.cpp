@@ -355,16 +355,74 @@ struct Checkpoint {
 // --full-wgs driver: reader threads fill read slabs, a bounded queue hands
 // chunks to one host thread per GPU (own msw_ctx), results are summed per file.
 // ---------------------------------------------------------------------------
-struct Chunk {
-    size_t file_index;
-    std::vector<uint8_t> reads;   // n x kReadStride
-    std::vector<uint16_t> rlen;
-    std::vector<int64_t> pos;
-    uint64_t n = 0;
-    bool last = false;            // last chunk of its file
+constexpr uint32_t kReadStride = 256;
+
+// Read slabs in pinned memory (msw_host_alloc = hipHostMalloc): the FASTQ
+// readers parse straight into them and msw_align_reads DMAs them to the GPU
+// without staging.  Recycled through a free list; one block per slab:
+// [reads cap x kReadStride | pos i64 x cap | rlen u16 x cap].
+class SlabPool {
+   public:
+    struct Slab {
+        uint8_t* base = nullptr;
+        uint8_t* reads = nullptr;
+        int64_t* pos = nullptr;
+        uint16_t* rlen = nullptr;
+        bool pinned = false;
+    };
+    explicit SlabPool(uint64_t cap) : cap_(cap) {}
+    ~SlabPool() {
+        for (Slab* s : free_) release(s);
+    }
+    Slab* get() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            if (!free_.empty()) {
+                Slab* s = free_.back();
+                free_.pop_back();
+                return s;
+            }
+        }
+        Slab* s = new Slab();
+        const size_t bytes = cap_ * (kReadStride + 8 + 2);
+        s->base = (uint8_t*)msw_host_alloc(bytes);
+        s->pinned = s->base != nullptr;
+        if (!s->base) s->base = (uint8_t*)malloc(bytes);  // pageable fallback: staged by the runtime
+        if (!s->base) die("error: out of host memory for read slabs");
+        s->reads = s->base;
+        s->pos = (int64_t*)(s->base + cap_ * kReadStride);
+        s->rlen = (uint16_t*)(s->base + cap_ * (kReadStride + 8));
+        return s;
+    }
+    void put(Slab* s) {
+        std::lock_guard<std::mutex> lk(m_);
+        free_.push_back(s);
+    }
+
+   private:
+    static void release(Slab* s) {
+        if (s->pinned) msw_host_free(s->base);
+        else free(s->base);
+        delete s;
+    }
+    uint64_t cap_;
+    std::mutex m_;
+    std::vector<Slab*> free_;
 };
 
-constexpr uint32_t kReadStride = 256;
+struct Chunk {
+    size_t file_index = 0;
+    SlabPool* pool = nullptr;
+    SlabPool::Slab* slab = nullptr;  // reads n x kReadStride, rlen, pos
+    uint64_t n = 0;
+    bool last = false;               // last chunk of its file
+    const uint8_t* reads() const { return slab->reads; }
+    const uint16_t* rlen() const { return slab->rlen; }
+    const int64_t* pos() const { return slab->pos; }
+    ~Chunk() {
+        if (slab) pool->put(slab);
+    }
+};
 
 struct FileState {
     std::string path;
@@ -441,6 +499,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         }
     }
     ChunkQueue queue(2 * (size_t)ngpu + 2);
+    SlabPool slabs(chunk);
     std::mutex ck_mu;
     std::atomic<unsigned long long> cells{0};
     const auto t_all = Clock::now();
@@ -495,11 +554,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 for (;;) {
                     std::unique_ptr<Chunk> c(new Chunk());
                     c->file_index = fi;
-                    c->reads.resize(chunk * kReadStride);
-                    c->rlen.resize(chunk);
-                    c->pos.resize(chunk);
-                    if (msw_fastq_next(fq, c->reads.data(), c->rlen.data(), kReadStride, chunk, &c->n,
-                                       c->pos.data()) != MSW_OK) {
+                    c->pool = &slabs;
+                    c->slab = slabs.get();
+                    if (msw_fastq_next(fq, c->slab->reads, c->slab->rlen, kReadStride, chunk, &c->n,
+                                       c->slab->pos) != MSW_OK) {
                         f.error = msw_last_error();
                         fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
                         f.failed = true;
@@ -564,7 +622,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 if (!c) break;
                 FileState& f = *st[c->file_index];
                 unsigned long long nb = 0;
-                for (uint64_t i = 0; i < c->n; ++i) nb += c->rlen[i];
+                for (uint64_t i = 0; i < c->n; ++i) nb += c->rlen()[i];
                 if (sw) {
                     // window = reference[pos : pos + W] (W = --window or 2 x read
                     // length, at most the kernel's 4096), clipped at the genome end
@@ -575,13 +633,13 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     fl->ei.assign(c->n, 0);
                     fl->ej.assign(c->n, 0);
                     for (uint64_t i = 0; i < c->n; ++i) {
-                        const uint32_t w = std::min<uint32_t>(a.window > 0 ? (uint32_t)a.window : 2u * c->rlen[i], 4096u);
+                        const uint32_t w = std::min<uint32_t>(a.window > 0 ? (uint32_t)a.window : 2u * c->rlen()[i], 4096u);
                         fl->want[i] = (uint16_t)w;
-                        const int64_t p = c->pos[i];
+                        const int64_t p = c->pos()[i];
                         if (p >= 0 && (uint64_t)p < genome.size())
-                            fl->cells += (unsigned long long)std::min<uint64_t>(w, genome.size() - (uint64_t)p) * c->rlen[i];
+                            fl->cells += (unsigned long long)std::min<uint64_t>(w, genome.size() - (uint64_t)p) * c->rlen()[i];
                     }
-                    msw_read_batch_t rb{c->reads.data(), c->rlen.data(), kReadStride, c->pos.data(), fl->want.data(), c->n};
+                    msw_read_batch_t rb{c->reads(), c->rlen(), kReadStride, c->pos(), fl->want.data(), c->n};
                     msw_out_t o{fl->score.data(), fl->ei.data(), fl->ej.data()};
                     fl->c = std::move(c);
                     if (msw_align_reads_async(ctx.h, &sc, gen, &rb, &o, 0, &fl->ticket) != MSW_OK) {
@@ -595,7 +653,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     long long chunk_score = 0;
                     std::string cat;
                     cat.reserve(nb);
-                    for (uint64_t i = 0; i < c->n; ++i) cat.append((const char*)c->reads.data() + i * kReadStride, c->rlen[i]);
+                    for (uint64_t i = 0; i < c->n; ++i) cat.append((const char*)c->reads() + i * kReadStride, c->rlen()[i]);
                     if (cat.size() >= 1000) {
                         int32_t s = 0;
                         if (msw_align_compat(ctx.h, (const uint8_t*)cat.data(), cat.size(), (const uint8_t*)cat.data(),
