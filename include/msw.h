@@ -169,7 +169,8 @@ uint64_t msw_genome_length(const msw_genome* g);
 /* Reads against genome windows: pair p scores reads[p*read_stride ..][0,
  * read_len[p]) against genome[win_pos[p], win_pos[p] + win_len[p]), the
  * window clipped at the genome end; win_pos < 0 or >= the genome length is an
- * empty window (score 0, coordinates (-1,-1)).  Host arrays as in
+ * empty window (score 0, coordinates (-1,-1)).  The requested win_len is
+ * bounded like a window length (<= 4096).  Host arrays as in
  * msw_align_batch (pageable or msw_host_alloc'ed: pinned arrays are copied to
  * the GPU directly, without staging). */
 typedef struct {

@@ -165,7 +165,7 @@ struct Slot {
     uint16_t *d_rlen = nullptr, *d_wlen = nullptr, *h_rlen = nullptr, *h_wlen = nullptr;
     int32_t *d_score = nullptr, *h_score = nullptr;
     int16_t *d_ei = nullptr, *d_ej = nullptr, *h_ei = nullptr, *h_ej = nullptr;
-    hipEvent_t uploaded = nullptr, done = nullptr;
+    hipEvent_t uploaded = nullptr, computed = nullptr, done = nullptr;
     bool busy = false;
     uint64_t ticket = 0;  // msw_align_*_async call that owns the chunk in flight
     // Pending readback bookkeeping.
@@ -206,7 +206,7 @@ void free_slot(Slot& s) {
 struct msw_ctx {
     int device = 0;
     int cu_count = 256;
-    hipStream_t compute = nullptr, copy = nullptr;
+    hipStream_t compute = nullptr, copy = nullptr, d2h = nullptr;
     Slot slots[2];
     uint64_t next_ticket = 1, done_ticket = 0;
     uint64_t slot_seq = 0;  // chunks submitted (slot = slot_seq & 1)
@@ -255,6 +255,7 @@ int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
     int rc;
     if (!s.uploaded) {
         HIP_TRY(hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s.computed, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     }
     if (pairs > s.cap_pairs) {
@@ -560,8 +561,9 @@ inline uint32_t round16(uint32_t v) { return (v + 15u) & ~15u; }
 // Window length actually scored in genome mode: clipped at the genome end,
 // empty for positions outside it.
 inline uint16_t genome_window(int64_t pos, uint16_t want, uint64_t glen) {
-    if (pos < 0 || (uint64_t)pos >= glen) return 0;
-    return (uint16_t)std::min<uint64_t>(want, glen - (uint64_t)pos);
+    const uint64_t p = (uint64_t)pos;  // negative positions wrap past glen
+    const uint64_t room = p < glen ? glen - p : 0;
+    return (uint16_t)std::min<uint64_t>(want, room);
 }
 
 // Copy `n` rows of `len` bytes from stride `src_stride` to `dst_stride`.
@@ -605,14 +607,11 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     if ((rc = set_device(ctx))) return rc;
     HostTrace tr;
     // Host-side range checks over the whole batch first: fail before any launch.
+    // (genome mode bounds the requested window lengths: a clipped window is
+    // never longer, and the positions need not be read here)
     uint32_t gm = 0, gn = 0;
     for (uint64_t i = 0; i < n; ++i) gm = std::max<uint32_t>(gm, b.read_len[i]);
-    if (gmode) {
-        for (uint64_t i = 0; i < n; ++i)
-            gn = std::max<uint32_t>(gn, genome_window(b.win_pos[i], b.win_len[i], b.genome->len));
-    } else {
-        for (uint64_t i = 0; i < n; ++i) gn = std::max<uint32_t>(gn, b.win_len[i]);
-    }
+    for (uint64_t i = 0; i < n; ++i) gn = std::max<uint32_t>(gn, b.win_len[i]);
     if (gm > b.read_stride || (!gmode && gn > b.win_stride))
         return fail(MSW_E_INVALID, "length exceeds stride (max read %u / stride %u, max window %u / stride %u)",
                     gm, b.read_stride, gn, b.win_stride);
@@ -633,8 +632,11 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     const bool multi_chunk = n > chunk || !sync;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
-    for (uint64_t first = 0; first < n; first += chunk, ++c) {
-        const uint64_t cnt = std::min(chunk, n - first);
+    for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
+        // A short first chunk starts the GPU early; the rest overlap (2-deep).
+        const uint64_t want = (c == 0 && n > chunk) ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8)
+                                                    : chunk;
+        cnt = std::min(want, n - first);
         // Slots alternate across calls too, so consecutive async calls overlap.
         Slot& s = ctx->slots[ctx->slot_seq++ & 1];
         if (tr.on) tr.submit += tr.lap();
@@ -689,20 +691,29 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
         const size_t meta_lo = gmode ? 0 : (uniform ? 12 : 8) * cnt;
         HIP_TRY(hipMemcpyAsync(s.d_meta + meta_lo, s.h_meta + meta_lo, kMetaBytesPerPair * cnt - meta_lo,
                                hipMemcpyHostToDevice, up));
+        // Pipelined: H2D + window cut on the copy stream, the scoring launch on
+        // the compute stream, results back on the d2h stream -- chunk k+1's
+        // uploads and chunk k-1's readback overlap chunk k's kernel.
+        if (gmode)
+            HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, s.d_pos, s.d_wlen, s.d_wins, ws, cnt, up));
         if (multi_chunk) {
             HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
             HIP_TRY(hipStreamWaitEvent(ctx->compute, s.uploaded, 0));
         }
-        if (gmode)
-            HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, s.d_pos, s.d_wlen, s.d_wins, ws, cnt, ctx->compute));
         if (uniform) {
             buckets.resize(1);
             buckets[0].begin = 0;
         }
         if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws))) return rc;
+        hipStream_t down = ctx->compute;
+        if (multi_chunk) {
+            HIP_TRY(hipEventRecord(s.computed, ctx->compute));
+            HIP_TRY(hipStreamWaitEvent(ctx->d2h, s.computed, 0));
+            down = ctx->d2h;
+        }
         HIP_TRY(hipMemcpyAsync(s.h_res, s.d_res, (sch.coords ? kResBytesPerPair : 4) * cnt, hipMemcpyDeviceToHost,
-                               ctx->compute));
-        HIP_TRY(hipEventRecord(s.done, ctx->compute));
+                               down));
+        HIP_TRY(hipEventRecord(s.done, down));
         s.busy = true;
         s.ticket = ctx->next_ticket;  // the ticket an async call returns
         s.first = first;
@@ -808,6 +819,7 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
         c->cu_count = prop.multiProcessorCount;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         return fail(MSW_E_DEVICE, "context creation on device %d failed: %s", ordinal, hipGetErrorString(e));
@@ -821,8 +833,10 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->compute) (void)hipStreamSynchronize(ctx->compute);
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
+    if (ctx->d2h) (void)hipStreamSynchronize(ctx->d2h);
     for (Slot& s : ctx->slots) {
         if (s.uploaded) (void)hipEventDestroy(s.uploaded);
+        if (s.computed) (void)hipEventDestroy(s.computed);
         if (s.done) (void)hipEventDestroy(s.done);
         free_slot(s);
     }
@@ -831,6 +845,7 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     (void)hipFree(ctx->c_res);
     if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
+    if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
     delete ctx;
 }
 
@@ -1178,6 +1193,7 @@ int msw_synchronize(msw_ctx* ctx) {
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->compute));
     HIP_TRY(hipStreamSynchronize(ctx->copy));
+    HIP_TRY(hipStreamSynchronize(ctx->d2h));
     HIP_TRY(hipGetLastError());
     return MSW_OK;
 }
