@@ -4,7 +4,10 @@
 // header.  One reader per lane file; no per-line allocation: records are
 // parsed out of a 4 MiB decompressed block buffer and sequences are copied
 // straight into the caller's SoA slab.
+#include <dlfcn.h>
 #include <zlib.h>
+
+#include <mutex>
 
 #include <cstdarg>
 #include <cstdint>
@@ -26,6 +29,10 @@ using msw_detail::set_error;
 
 struct msw_fastq {
     gzFile gz = nullptr;      // zlib reads plain files transparently too
+    FILE* raw = nullptr;      // BGZF files decoded block by block with libdeflate
+    void* inflater = nullptr; // libdeflate_decompressor (BGZF mode)
+    std::vector<unsigned char> cblock;  // one compressed BGZF block
+    std::string io_msg;       // last BGZF decode error
     std::vector<char> buf;    // decompressed bytes
     size_t head = 0, tail = 0;
     bool eof = false;
@@ -39,6 +46,92 @@ struct msw_fastq {
 namespace {
 
 constexpr size_t kBlock = 4u << 20;
+
+// ---------------------------------------------------------------------------
+// BGZF lane files (multi-member gzip whose members are <= 64 KiB blocks with a
+// 'BC' extra field carrying the block size, as written by bgzip) are inflated
+// block by block with libdeflate (the image's libdeflate.so.0, loaded at run
+// time; ~2-3x zlib's inflate rate).  Any other gzip -- and every file when
+// libdeflate is absent or MSW_NO_LIBDEFLATE is set -- streams through zlib.
+// Both paths yield the same bytes (tests/test_fastq.py).
+// ---------------------------------------------------------------------------
+struct Deflate {
+    void* (*alloc)() = nullptr;
+    int (*decompress)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
+    void (*free_)(void*) = nullptr;
+    uint32_t (*crc32)(uint32_t, const void*, size_t) = nullptr;
+    bool ok = false;
+};
+
+const Deflate& libdeflate() {
+    static Deflate d;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        d.alloc = (void* (*)())dlsym(h, "libdeflate_alloc_decompressor");
+        d.decompress = (int (*)(void*, const void*, size_t, void*, size_t, size_t*))dlsym(h, "libdeflate_deflate_decompress");
+        d.free_ = (void (*)(void*))dlsym(h, "libdeflate_free_decompressor");
+        d.crc32 = (uint32_t(*)(uint32_t, const void*, size_t))dlsym(h, "libdeflate_crc32");
+        d.ok = d.alloc && d.decompress && d.free_ && d.crc32;
+    });
+    return d;
+}
+
+// Size of the BGZF block whose 18-byte header is h, or 0 if h is not one.
+size_t bgzf_block_size(const unsigned char* h) {
+    if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return 0;
+    const unsigned xlen = h[10] | (h[11] << 8);
+    if (xlen != 6 || h[12] != 'B' || h[13] != 'C' || (h[14] | (h[15] << 8)) != 2) return 0;
+    return (size_t)(h[16] | (h[17] << 8)) + 1;
+}
+
+bool is_bgzf(const char* path) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return false;
+    unsigned char h[18];
+    const bool yes = fread(h, 1, 18, f) == 18 && bgzf_block_size(h) >= 26;
+    fclose(f);
+    return yes;
+}
+
+// Inflate whole BGZF blocks into out[0, cap) while another block surely fits
+// (a block holds <= 64 KiB); returns bytes produced, 0 at end of file, -1 on
+// a read / format / checksum error (fq->io_msg says which).
+long bgzf_fill(msw_fastq* fq, char* out, size_t cap) {
+    const Deflate& d = libdeflate();
+    size_t n = 0;
+    while (n + 65536 <= cap) {
+        unsigned char h[18];
+        const size_t got = fread(h, 1, 18, fq->raw);
+        if (got == 0 && feof(fq->raw)) break;
+        const size_t bsize = got == 18 ? bgzf_block_size(h) : 0;
+        if (bsize < 26) {
+            fq->io_msg = "not a BGZF block (mixed gzip members are not supported in BGZF mode)";
+            return -1;
+        }
+        fq->cblock.resize(bsize - 18);
+        if (fread(fq->cblock.data(), 1, bsize - 18, fq->raw) != bsize - 18) {
+            fq->io_msg = "unexpected end of file";
+            return -1;
+        }
+        const unsigned char* t = fq->cblock.data() + bsize - 26;
+        const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
+        const uint32_t isize = t[4] | (t[5] << 8) | (t[6] << 16) | ((uint32_t)t[7] << 24);
+        if (isize > 65536) {
+            fq->io_msg = "BGZF block larger than 64 KiB";
+            return -1;
+        }
+        size_t actual = 0;
+        if (d.decompress(fq->inflater, fq->cblock.data(), bsize - 26, out + n, isize, &actual) != 0 || actual != isize ||
+            d.crc32(0, out + n, isize) != crc) {
+            fq->io_msg = "invalid compressed data";
+            return -1;
+        }
+        n += isize;
+    }
+    return (long)n;
+}
 
 // Strict UTF-8 validation (what Rust's String conversion in lines() checks).
 bool valid_utf8(const unsigned char* s, size_t n) {
@@ -119,7 +212,8 @@ bool next_line(msw_fastq* fq, const char** line, size_t* len, int* io_err) {
             *len = fq->last.size();
             return true;
         }
-        const int got = gzread(fq->gz, fq->buf.data(), (unsigned)kBlock);
+        const long got = fq->raw ? bgzf_fill(fq, fq->buf.data(), kBlock)
+                                 : (long)gzread(fq->gz, fq->buf.data(), (unsigned)kBlock);
         if (got < 0) {
             *io_err = 1;
             return false;
@@ -140,7 +234,7 @@ int next_sequence(msw_fastq* fq, const char** seq, size_t* len, int64_t* pos, bo
         if (!next_line(fq, &line, &n, &io_err)) {
             if (!io_err) return 0;
             int zerr = 0;
-            const char* msg = gzerror(fq->gz, &zerr);
+            const char* msg = fq->raw ? fq->io_msg.c_str() : gzerror(fq->gz, &zerr);
             if (++fq->errors > 10)
                 return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
                                  (unsigned long long)fq->lines);
@@ -175,11 +269,24 @@ extern "C" {
 int msw_fastq_open(const char* path, msw_fastq** out) {
     if (!path || !out) return set_error(MSW_E_INVALID, "path/out is NULL");
     *out = nullptr;
-    gzFile gz = gzopen(path, "rb");
-    if (!gz) return set_error(MSW_E_INVALID, "Failed to open file %s", path);
-    gzbuffer(gz, 1u << 20);
     msw_fastq* fq = new msw_fastq();
-    fq->gz = gz;
+    const Deflate& d = libdeflate();
+    if (d.ok && !getenv("MSW_NO_LIBDEFLATE") && is_bgzf(path)) {
+        fq->raw = fopen(path, "rb");
+        fq->inflater = fq->raw ? d.alloc() : nullptr;
+        if (fq->raw) setvbuf(fq->raw, nullptr, _IOFBF, 1u << 20);
+    }
+    if (!fq->inflater) {
+        if (fq->raw) fclose(fq->raw);
+        fq->raw = nullptr;
+        gzFile gz = gzopen(path, "rb");
+        if (!gz) {
+            delete fq;
+            return set_error(MSW_E_INVALID, "Failed to open file %s", path);
+        }
+        gzbuffer(gz, 1u << 20);
+        fq->gz = gz;
+    }
     fq->buf.resize(kBlock);
     fq->path = path;
     *out = fq;
@@ -189,6 +296,8 @@ int msw_fastq_open(const char* path, msw_fastq** out) {
 void msw_fastq_close(msw_fastq* fq) {
     if (!fq) return;
     if (fq->gz) gzclose(fq->gz);
+    if (fq->raw) fclose(fq->raw);
+    if (fq->inflater) libdeflate().free_(fq->inflater);
     delete fq;
 }
 

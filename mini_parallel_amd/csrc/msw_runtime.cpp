@@ -790,6 +790,9 @@ int msw_device_info(int ordinal, msw_device_info_t* out) {
     HIP_TRY(hipGetDeviceProperties(&prop, ordinal));
     memset(out, 0, sizeof(*out));
     snprintf(out->name, sizeof(out->name), "%s", prop.name);
+    if (!out->name[0])  // the marketing name can be empty under ROCm: name the target instead
+        snprintf(out->name, sizeof(out->name), "AMD Instinct GPU (%s, %d CUs)", prop.gcnArchName,
+                 prop.multiProcessorCount);
     snprintf(out->arch, sizeof(out->arch), "%s", prop.gcnArchName);
     out->mem_bytes = prop.totalGlobalMem;
     out->max_wg = (uint32_t)prop.maxThreadsPerBlock;

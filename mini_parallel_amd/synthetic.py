@@ -111,10 +111,33 @@ def config_batch(k: int, n_pairs: int = 0, seed_offset: int = 0) -> PairBatch:
     raise ValueError(f"unknown config {k}")
 
 
+BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def bgzf_compress(data: bytes, level: int = 1) -> bytes:
+    """BGZF (bgzip's block gzip): a multi-member gzip of <= 64 KiB blocks whose
+    'BC' extra field holds the block size, then the empty EOF block.  Any gzip
+    reader (zcat, the reference's lane loader) reads it as one stream; the C++
+    reader inflates it block by block with libdeflate."""
+    import struct
+    import zlib
+    out = []
+    for k in range(0, len(data), 0xFF00):
+        chunk = data[k:k + 0xFF00]
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        cdata = c.compress(chunk) + c.flush()
+        out.append(struct.pack("<4BIBBH2BHH", 0x1F, 0x8B, 8, 4, 0, 0, 0xFF, 6, ord("B"), ord("C"), 2,
+                               len(cdata) + 25))
+        out.append(cdata)
+        out.append(struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+    out.append(BGZF_EOF)
+    return b"".join(out)
+
+
 def _write_lane_file(job):
     """One lane file of write_wgs_dataset (a process-pool job)."""
     import gzip
-    (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep) = job
+    (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep, bgzf) = job
     genome_bases = int(g.shape[0])
     b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_arr=g,
                    read_stride=(read_len + 16 + 15) // 16 * 16)
@@ -128,8 +151,12 @@ def _write_lane_file(job):
     tag = sample.encode()
     recs = [b"@%s:%d:%d pos=%d\n%s\n+\n%s\n" % (tag, lane, i, int(pos[i]), b.reads[i, :rl[i]].tobytes(),
                                                   qual[:rl[i]]) for i in range(b.n_pairs)]
-    with gzip.open(name, "wb", compresslevel=compresslevel) as f:
-        f.write(b"".join(recs))
+    if bgzf:
+        with open(name, "wb") as f:
+            f.write(bgzf_compress(b"".join(recs), compresslevel))
+    else:
+        with gzip.open(name, "wb", compresslevel=compresslevel) as f:
+            f.write(b"".join(recs))
     if not keep:
         return None
     cols = np.arange(b.wins.shape[1])
@@ -141,13 +168,13 @@ def _write_lane_file(job):
 def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_per_lane: int = 2,
                       reads_per_file: int = 1000, read_len: int = 150, win_factor: float = 2.0,
                       seed: int = 1004, genome_bases: int = 1 << 20, keep_batches: bool = True,
-                      compresslevel: int = 1, workers: int = 1) -> dict:
+                      compresslevel: int = 1, workers: int = 1, bgzf: bool = False) -> dict:
     """Config-4-shaped dataset: lane files {sample}_L{lane:03}_R{r}_001.fastq.gz
     (aligner.rs:198-204 naming) whose headers carry "pos=<window start>", and
     the reference genome as reference.fa.  Returns paths and (keep_batches) the
     pair batches (reads, windows) so tests can score them with the oracle.
     Vectorised, and ``workers`` > 1 writes the lane files in parallel processes
-    (same files either way)."""
+    (same files either way).  ``bgzf`` writes block-gzip (bgzip) lane files."""
     import os
     os.makedirs(out_dir, exist_ok=True)
     rng = np.random.default_rng(seed)
@@ -162,7 +189,7 @@ def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_p
         for r in range(1, reads_per_lane + 1):
             name = os.path.join(out_dir, "%s_L%03d_R%d_001.fastq.gz" % (sample, lane, r))
             jobs.append((g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel,
-                         keep_batches))
+                         keep_batches, bgzf))
             files.append(name)
             k += 1
     if workers > 1 and len(jobs) > 1:

@@ -132,3 +132,37 @@ def test_empty_file(tmp_path):
     got = []
     process_fastq_file_in_chunks(p, 10, got.append)
     assert got == [] and count_bases_in_fastq(p) == 0
+
+
+@pytest.mark.parametrize("no_libdeflate", [False, True])
+@pytest.mark.parametrize("crlf", [False, True])
+def test_bgzf_lane_file(tmp_path, monkeypatch, no_libdeflate, crlf):
+    """Block-gzip (bgzip) lane files: inflated block by block with libdeflate
+    (or by zlib with MSW_NO_LIBDEFLATE): same chunks as the restatement, with
+    records split across 64 KiB block boundaries."""
+    from mini_parallel_amd.synthetic import bgzf_compress
+    if no_libdeflate:
+        monkeypatch.setenv("MSW_NO_LIBDEFLATE", "1")
+    rng = np.random.default_rng(9)
+    data = synth_fastq(3000, rng, crlf=crlf)
+    p = str(tmp_path / "b.fastq.gz")
+    open(p, "wb").write(bgzf_compress(data))
+    assert gzip.decompress(open(p, "rb").read()) == data
+    got = []
+    process_fastq_file_in_chunks(p, 333, got.append)
+    assert got == reference_chunks(data, 333)
+    assert count_bases_in_fastq(p) == sum(len(s) for c in got for s in c)
+    with FastqReader(p) as fq:
+        seqs, lens, pos = fq.next_chunk(5000, stride=304, with_pos=True)
+    assert list(pos) == [i * 7 for i in range(3000)]
+
+
+def test_bgzf_corrupt_block_is_an_error(tmp_path):
+    from mini_parallel_amd.synthetic import bgzf_compress
+    rng = np.random.default_rng(10)
+    blob = bytearray(bgzf_compress(synth_fastq(2000, rng)))
+    blob[70000] ^= 0xFF  # inside the second block's deflate data
+    p = str(tmp_path / "c.fastq.gz")
+    open(p, "wb").write(bytes(blob))
+    with pytest.raises(MswError):
+        process_fastq_file_in_chunks(p, 100000, lambda c: None)

@@ -32,13 +32,14 @@ def main():
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--out", default="gpurun_out/wgs_e2e.jsonl")
     ap.add_argument("--extra-env", default="", help="K=V,K=V added to the CLI's environment")
+    ap.add_argument("--bgzf", action="store_true", help="write block-gzip (bgzip) lane files")
     args = ap.parse_args()
 
     from mini_parallel_amd.synthetic import write_wgs_dataset
     t0 = time.time()
     ds = write_wgs_dataset(args.dir, lanes=args.lanes, reads_per_lane=args.reads_per_lane,
                            reads_per_file=args.reads_per_file, genome_bases=args.genome_bases,
-                           keep_batches=False, workers=args.workers)
+                           keep_batches=False, workers=args.workers, bgzf=args.bgzf)
     gen_s = time.time() - t0
     gz_bytes = sum(os.path.getsize(f) for f in ds["files"])
     print(f"dataset: {len(ds['files'])} files, {gz_bytes / 1e6:.0f} MB gz, written in {gen_s:.1f} s", flush=True)
@@ -62,7 +63,7 @@ def main():
             raise SystemExit(f"CLI failed with {r.returncode}")
         d = json.load(open(rec))
         d.update({"readers": readers, "process_wall_s": round(wall, 3), "gz_bytes": gz_bytes,
-                  "chunk_reads": args.chunk, "extra_env": args.extra_env,
+                  "chunk_reads": args.chunk, "extra_env": args.extra_env, "bgzf": args.bgzf,
                   "dataset": f"{args.lanes} lanes x {args.reads_per_lane} files x {args.reads_per_file} "
                              f"150 bp reads, {args.genome_bases} bp genome, window 300"})
         print(json.dumps(d), flush=True)
