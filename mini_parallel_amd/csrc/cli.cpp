@@ -527,10 +527,18 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     // Readers: one thread per lane file in flight (a gzip stream inflates on
     // one core; zlib gives ~0.5-0.75 M reads/s per thread, far below what one
     // GPU scores, so the host side wants every file open at once).  Default
-    // min(files, 16) -- the box's CPU share -- or MSW_READERS.
+    // min(files, MSW_HOST_THREADS) -- the host CPU share, default 16 -- or
+    // MSW_READERS.
     std::atomic<size_t> next_file{0};
-    const int want_readers = atoi(env_or("MSW_READERS", "16").c_str());
+    const int host_threads = std::max(1, atoi(env_or("MSW_HOST_THREADS", "16").c_str()));
+    const int want_readers = std::max(1, atoi(env_or("MSW_READERS", std::to_string(host_threads).c_str()).c_str()));
     const int nreaders = std::max(1, std::min<int>((int)todo.size(), std::max(want_readers, 2 * ngpu)));
+    // Fewer files than the CPU share: BGZF blocks of one file inflate on
+    // several threads (msw_fastq.cpp; MSW_INFLATE_THREADS overrides).
+    if (!getenv("MSW_INFLATE_THREADS")) {
+        const std::string per = std::to_string(std::max(1, host_threads / nreaders));
+        setenv("MSW_INFLATE_THREADS", per.c_str(), 0);
+    }
     std::vector<std::thread> readers;
     std::atomic<int> readers_left{nreaders};
     for (int r = 0; r < nreaders; ++r) {

@@ -7,7 +7,10 @@
 #include <dlfcn.h>
 #include <zlib.h>
 
+#include <algorithm>
+#include <atomic>
 #include <mutex>
+#include <thread>
 
 #include <cstdarg>
 #include <cstdint>
@@ -30,7 +33,7 @@ using msw_detail::set_error;
 struct msw_fastq {
     gzFile gz = nullptr;      // zlib reads plain files transparently too
     FILE* raw = nullptr;      // BGZF files decoded block by block with libdeflate
-    void* inflater = nullptr; // libdeflate_decompressor (BGZF mode)
+    std::vector<void*> inflaters;  // libdeflate decompressors, one per inflate thread (BGZF mode)
     std::vector<unsigned char> cblock;  // one compressed BGZF block
     std::string io_msg;       // last BGZF decode error
     std::vector<char> buf;    // decompressed bytes
@@ -97,9 +100,18 @@ bool is_bgzf(const char* path) {
 
 // Inflate whole BGZF blocks into out[0, cap) while another block surely fits
 // (a block holds <= 64 KiB); returns bytes produced, 0 at end of file, -1 on
-// a read / format / checksum error (fq->io_msg says which).
+// a read / format / checksum error (fq->io_msg says which).  The compressed
+// blocks are read first (each trailer gives its output size, hence its output
+// offset), then inflated -- by fq->inflaters.size() threads when the reader
+// was opened with MSW_INFLATE_THREADS > 1.
 long bgzf_fill(msw_fastq* fq, char* out, size_t cap) {
     const Deflate& d = libdeflate();
+    struct Blk {
+        size_t coff, clen, ooff;
+        uint32_t isize, crc;
+    };
+    std::vector<Blk> blks;
+    fq->cblock.clear();
     size_t n = 0;
     while (n + 65536 <= cap) {
         unsigned char h[18];
@@ -110,25 +122,41 @@ long bgzf_fill(msw_fastq* fq, char* out, size_t cap) {
             fq->io_msg = "not a BGZF block (mixed gzip members are not supported in BGZF mode)";
             return -1;
         }
-        fq->cblock.resize(bsize - 18);
-        if (fread(fq->cblock.data(), 1, bsize - 18, fq->raw) != bsize - 18) {
+        const size_t at = fq->cblock.size();
+        fq->cblock.resize(at + bsize - 18);
+        if (fread(fq->cblock.data() + at, 1, bsize - 18, fq->raw) != bsize - 18) {
             fq->io_msg = "unexpected end of file";
             return -1;
         }
-        const unsigned char* t = fq->cblock.data() + bsize - 26;
+        const unsigned char* t = fq->cblock.data() + at + bsize - 26;
         const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
         const uint32_t isize = t[4] | (t[5] << 8) | (t[6] << 16) | ((uint32_t)t[7] << 24);
         if (isize > 65536) {
             fq->io_msg = "BGZF block larger than 64 KiB";
             return -1;
         }
-        size_t actual = 0;
-        if (d.decompress(fq->inflater, fq->cblock.data(), bsize - 26, out + n, isize, &actual) != 0 || actual != isize ||
-            d.crc32(0, out + n, isize) != crc) {
-            fq->io_msg = "invalid compressed data";
-            return -1;
-        }
+        if (isize) blks.push_back({at, bsize - 26, n, isize, crc});
         n += isize;
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<bool> bad{false};
+    auto work = [&](void* inflater) {
+        for (size_t k; (k = next.fetch_add(1)) < blks.size();) {
+            const Blk& bk = blks[k];
+            size_t actual = 0;
+            if (d.decompress(inflater, fq->cblock.data() + bk.coff, bk.clen, out + bk.ooff, bk.isize, &actual) != 0 ||
+                actual != bk.isize || d.crc32(0, out + bk.ooff, bk.isize) != bk.crc)
+                bad = true;
+        }
+    };
+    const size_t nt = std::min(fq->inflaters.size(), blks.size());
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < nt; ++t) pool.emplace_back(work, fq->inflaters[t]);
+    work(fq->inflaters[0]);
+    for (auto& th : pool) th.join();
+    if (bad) {
+        fq->io_msg = "invalid compressed data";
+        return -1;
     }
     return (long)n;
 }
@@ -273,10 +301,13 @@ int msw_fastq_open(const char* path, msw_fastq** out) {
     const Deflate& d = libdeflate();
     if (d.ok && !getenv("MSW_NO_LIBDEFLATE") && is_bgzf(path)) {
         fq->raw = fopen(path, "rb");
-        fq->inflater = fq->raw ? d.alloc() : nullptr;
+        const char* nt = getenv("MSW_INFLATE_THREADS");
+        const int threads = std::max(1, std::min(64, nt ? atoi(nt) : 1));
+        for (int t = 0; fq->raw && t < threads; ++t)
+            if (void* inf = d.alloc()) fq->inflaters.push_back(inf);
         if (fq->raw) setvbuf(fq->raw, nullptr, _IOFBF, 1u << 20);
     }
-    if (!fq->inflater) {
+    if (fq->inflaters.empty()) {
         if (fq->raw) fclose(fq->raw);
         fq->raw = nullptr;
         gzFile gz = gzopen(path, "rb");
@@ -297,7 +328,7 @@ void msw_fastq_close(msw_fastq* fq) {
     if (!fq) return;
     if (fq->gz) gzclose(fq->gz);
     if (fq->raw) fclose(fq->raw);
-    if (fq->inflater) libdeflate().free_(fq->inflater);
+    for (void* inf : fq->inflaters) libdeflate().free_(inf);
     delete fq;
 }
 
