@@ -131,10 +131,13 @@ class Context:
 
     # -- batched scoring from host memory --------------------------------------------
     def align_batch(self, reads: np.ndarray, read_len: np.ndarray, wins: np.ndarray,
-                    win_len: np.ndarray, scoring: Scoring = LINEAR, chunk_pairs: int = 0):
+                    win_len: np.ndarray, scoring: Scoring = LINEAR, chunk_pairs: int = 0,
+                    asynchronous: bool = False):
         """Score a padded SoA batch (uint8 [B, stride] reads / windows, uint16
         lengths).  Returns (score int32[B], end_i int16[B], end_j int16[B]);
-        the coordinates are None unless ``scoring.want_coords``."""
+        the coordinates are None unless ``scoring.want_coords``.  With
+        ``asynchronous`` (msw_align_batch_async) it returns a :class:`Pending`
+        whose ``wait()`` gives the same tuple."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)
         wins = np.ascontiguousarray(wins, dtype=np.uint8)
         read_len = np.ascontiguousarray(read_len, dtype=np.uint16)
@@ -150,6 +153,11 @@ class Context:
                        wins.shape[1] if wins.ndim == 2 else 0, B)
         out = OutT(_ptr(score), _ptr(ei), _ptr(ej))
         sc = scoring.to_c()
+        if asynchronous:
+            t = ctypes.c_uint64(0)
+            check(lib().msw_align_batch_async(self.handle, ctypes.byref(sc), ctypes.byref(batch),
+                                              ctypes.byref(out), chunk_pairs, ctypes.byref(t)))
+            return Pending(self, t.value, (score, ei, ej), (reads, wins, read_len, win_len))
         check(lib().msw_align_batch(self.handle, ctypes.byref(sc), ctypes.byref(batch),
                                     ctypes.byref(out), chunk_pairs))
         return score, ei, ej
@@ -162,10 +170,11 @@ class Context:
 
     def align_reads(self, genome: "Genome", reads: np.ndarray, read_len: np.ndarray,
                     win_pos: np.ndarray, win_len: np.ndarray, scoring: Scoring = LINEAR,
-                    chunk_pairs: int = 0):
+                    chunk_pairs: int = 0, asynchronous: bool = False):
         """Score read p against genome[win_pos[p] : win_pos[p] + win_len[p]]
         (clipped at the genome end; positions outside it score 0).  Returns
-        (score, end_i, end_j) like :meth:`align_batch`."""
+        (score, end_i, end_j) like :meth:`align_batch` (a :class:`Pending`
+        with ``asynchronous``, msw_align_reads_async)."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)
         read_len = np.ascontiguousarray(read_len, dtype=np.uint16)
         win_pos = np.ascontiguousarray(win_pos, dtype=np.int64)
@@ -180,6 +189,12 @@ class Context:
                            _ptr(win_pos), _ptr(win_len), B)
         out = OutT(_ptr(score), _ptr(ei), _ptr(ej))
         sc = scoring.to_c()
+        if asynchronous:
+            t = ctypes.c_uint64(0)
+            check(lib().msw_align_reads_async(self.handle, ctypes.byref(sc), genome.handle,
+                                              ctypes.byref(batch), ctypes.byref(out), chunk_pairs,
+                                              ctypes.byref(t)))
+            return Pending(self, t.value, (score, ei, ej), (reads, read_len, win_pos, win_len, genome))
         check(lib().msw_align_reads(self.handle, ctypes.byref(sc), genome.handle, ctypes.byref(batch),
                                     ctypes.byref(out), chunk_pairs))
         return score, ei, ej
@@ -276,6 +291,21 @@ class Context:
         check(lib().msw_align_compat(self.handle, b1, len(s1), b2, len(s2), wg, max_groups,
                                      ctypes.byref(res)))
         return int(res.value)
+
+
+class Pending:
+    """An asynchronous call in flight (msw_*_async ticket).  The input arrays
+    are held until ``wait()``; ``wait()`` returns (score, end_i, end_j).
+    Waiting on a ticket also completes every earlier one (msw_wait)."""
+
+    def __init__(self, ctx: "Context", ticket: int, outs, keep):
+        self.ctx, self.ticket, self._outs, self._keep = ctx, ticket, outs, keep
+
+    def wait(self):
+        if self._keep is not None:
+            check(lib().msw_wait(self.ctx.handle, self.ticket))
+            self._keep = None
+        return self._outs
 
 
 class Genome:

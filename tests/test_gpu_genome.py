@@ -197,3 +197,23 @@ def test_pinned_genome_reads(gpu_ctx, oracle):
     got = gpu_ctx.align_reads(genome, pR, prl, ppos, pwant, sc, chunk_pairs=1500)
     W, wl = host_windows(g, pos, want)
     assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), True)
+
+
+def test_async_calls_in_flight(gpu_ctx, oracle):
+    """Several msw_*_async calls in flight on one context (slots alternate
+    across calls), waited in and out of order: every result bit-exact."""
+    g, R, rl, pos, want = genome_case(3000, 400_000, seed=61)
+    genome = gpu_ctx.load_genome(g)
+    sc = Scoring(want_coords=True)
+    W, wl = host_windows(g, pos, want)
+    expect = oracle_run(oracle, R, rl, W, wl, sc)
+    parts = [slice(0, 1000), slice(1000, 1700), slice(1700, 3000)]
+    pend = [gpu_ctx.align_reads(genome, R[p], rl[p], pos[p], want[p], sc, chunk_pairs=c, asynchronous=True)
+            for p, c in zip(parts, (0, 300, 512))]
+    pend.append(gpu_ctx.align_batch(R, rl, W, wl, sc, asynchronous=True))
+    got = [None] * 4
+    for k in (2, 0, 3, 1):  # waiting on a later ticket completes the earlier ones
+        got[k] = pend[k].wait()
+    for p, r in zip(parts, got[:3]):
+        assert_same(r, tuple(e[p] for e in expect), True)
+    assert_same(got[3], expect, True)
