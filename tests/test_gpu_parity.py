@@ -361,3 +361,24 @@ def test_full_size_properties(gpu_ctx, oracle):
     s_lin = gpu_run(gpu_ctx, b, Scoring())[0]
     s_lin_c = gpu_run(gpu_ctx, b, Scoring(want_coords=True))[0]
     assert np.array_equal(s_lin, s_lin_c)
+
+
+def test_config1_plumbing(gpu_ctx, oracle):
+    """BASELINE config 1: two 32 bp synthetic sequences (seed 1001) through the
+    batched path and through the CLI's pair mode (`-1 -2 --gpu --score-mode sw`),
+    against the oracle; the legacy pair mode against the compat restatement."""
+    import subprocess
+    b = config_batch(1)
+    sc = Scoring(want_coords=True)
+    want = oracle_run(oracle, b, sc)
+    assert_same(gpu_run(gpu_ctx, b, sc), want, True)
+    s1 = bytes(b.reads[0, :b.read_len[0]]).decode()
+    s2 = bytes(b.wins[0, :b.win_len[0]]).decode()
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mini_parallel_amd",
+                       "rustseq_mini")
+    out = subprocess.run([cli, "-1", s1, "-2", s2, "--gpu", "--score-mode", "sw"], capture_output=True, text=True,
+                         check=True).stdout
+    assert f"GPU Alignment score: {int(want[0][0])}" in out
+    assert f"Best cell: read {int(want[1][0])}, window {int(want[2][0])}" in out
+    out = subprocess.run([cli, "-1", s1, "-2", s2, "--gpu"], capture_output=True, text=True, check=True).stdout
+    assert f"GPU Alignment score: {oracle.compat_align(s1.encode(), s2.encode(), 1024, 1_000_000)}" in out
