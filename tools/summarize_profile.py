@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Summarise tools/profile_round.sh output into profiles/<round>/ and
-profiles/pmc_traffic.json (per-launch HBM bytes for bench.py's roofline).
+profiles/pmc_traffic.json (per-launch HBM bytes for bench.py's roofline,
+keyed "config<k>:<kind>" as bench.py looks them up).
 Usage: python tools/summarize_profile.py r01"""
 import csv
 import glob
@@ -11,6 +12,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KIND = {2: "linear", 3: "affine_coords", 5: "linear"}  # bench.py scoring per config
 
 
 def counters(path):
@@ -27,38 +29,37 @@ def main():
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
-    for f in glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True):
-        shutil.copy(f, os.path.join(dst, "kernel_stats_bench.csv"))
-    c = {}
-    for part in ("fetch", "write", "occ", "inst"):
-        c.update(counters(os.path.join(src, part)))
-    kernels = sorted({k for k, _ in c})
-    summary = {}
-    traffic = {}
-    for k in kernels:
-        d = {cn: v for (kn, cn), v in c.items() if kn == k}
-        summary[k] = d
-        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            fetch_b = d["FETCH_SIZE"] * 1024
-            write_b = d["WRITE_SIZE"] * 1024
-            traffic_entry = {
-                "fetch_bytes_raw": fetch_b, "write_bytes": write_b,
-                "hbm_bytes_per_launch": fetch_b * 2 + write_b,
-                "note": "FETCH_SIZE x 2 (gfx950 reports half of wide 16 B/lane reads, "
-                        "MI355X_MICROARCH.md HBM section) + WRITE_SIZE; per launch; batch is "
-                        "re-read every step and may be served from the 256 MiB Infinity Cache",
-            }
-            kind = "sw_kernel" if "sw_kernel" in k else ("sw_mixed_kernel" if "mixed" in k else k)
-            traffic[k] = traffic_entry
-            # tools/profile_round.sh profiles the default bench workload
-            traffic.setdefault("config2:linear", traffic_entry)
-        if "GRBM_GUI_ACTIVE" in d:
-            summary[k]["note_clock"] = "effective clock = GRBM_GUI_ACTIVE / 8 / kernel time"
+    summary, traffic = {}, {}
+    for cfg in (2, 3, 5):
+        d = os.path.join(src, f"c{cfg}")
+        if not os.path.isdir(d):
+            continue
+        for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
+            shutil.copy(f, os.path.join(dst, f"kernel_stats_config{cfg}.csv"))
+        c = {}
+        for part in ("fetch", "write", "occ", "inst"):
+            c.update(counters(os.path.join(d, part)))
+        per_kernel = {}
+        for k in sorted({k for k, _ in c}):
+            per_kernel[k] = {cn: v for (kn, cn), v in c.items() if kn == k}
+        summary[f"config{cfg}"] = per_kernel
+        # the dominant (scoring) kernel of the config
+        main_k = [k for k in per_kernel if "cut_windows" not in k]
+        for k in main_k:
+            m = per_kernel[k]
+            if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+                fetch_b, write_b = m["FETCH_SIZE"] * 1024, m["WRITE_SIZE"] * 1024
+                traffic[f"config{cfg}:{KIND[cfg]}"] = {
+                    "kernel": k, "fetch_bytes_raw": fetch_b, "write_bytes": write_b,
+                    "hbm_bytes_per_launch": fetch_b * 2 + write_b,
+                    "note": "FETCH_SIZE x 2 (gfx950 reports half of wide 16 B/lane reads, "
+                            "MI355X_MICROARCH.md HBM section) + WRITE_SIZE; per launch; the batch is "
+                            "re-read every step and may be served from the 256 MiB Infinity Cache"}
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
-    print(json.dumps(summary, indent=1))
+    print(json.dumps(traffic, indent=1))
 
 
 if __name__ == "__main__":
