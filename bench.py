@@ -266,6 +266,8 @@ def main():
 
     from mini_parallel_amd import dist as mdist
     wall_ms, kern_ms = mdist.max_over_ranks([wall_ms, kern_ms], device=dev)
+    # every rank scores its own shard: the job's cells are the sum over ranks
+    job_cells = mdist.sum_over_ranks([cells], device=dev)[0]
 
     # Final score/coordinate gather over RCCL (outside the timed region): the
     # only collective of the path.
@@ -276,7 +278,7 @@ def main():
     if rank == 0:
         gpu_scores = score.cpu().numpy()
         gpu_i, gpu_j = ei.cpu().numpy(), ej.cpu().numpy()
-        value = world * cells * args.steps / (wall_ms * 1e-3) / 1e9
+        value = job_cells * args.steps / (wall_ms * 1e-3) / 1e9
         ms_per_step = wall_ms / args.steps
         avg_launch_s = kern_ms * 1e-3 / args.steps
         alg_bytes = int(batch.read_len.astype(np.int64).sum() + batch.win_len.astype(np.int64).sum()

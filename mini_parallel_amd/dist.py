@@ -30,6 +30,16 @@ def max_over_ranks(values, device=None):
     return [float(x) for x in t.tolist()]
 
 
+def sum_over_ranks(values, device=None):
+    """Element-wise sum of a list of integers over all ranks (work counts)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(values), dtype=torch.int64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]
+
+
 def gather_results(*tensors):
     """Gather per-rank result tensors (equal or unequal lengths) to every rank,
     concatenated in rank order.  Unequal shards are padded to the longest and

@@ -29,11 +29,13 @@ def _worker(rank, world, port, n_total, out_dir):
     scores = torch.arange(a, b, dtype=torch.int32) * 3 + 1
     ei = torch.arange(a, b, dtype=torch.int16) % 7
     t = mdist.max_over_ranks([1.0 + rank, 5.0 - rank])
+    cells = mdist.sum_over_ranks([b - a, 10 ** 12 + rank])
     g_scores, g_ei = mdist.gather_results(scores, ei)
     if rank == 0:
         np.save(os.path.join(out_dir, "scores.npy"), g_scores.numpy())
         np.save(os.path.join(out_dir, "ei.npy"), g_ei.numpy())
         np.save(os.path.join(out_dir, "t.npy"), np.array(t))
+        np.save(os.path.join(out_dir, "cells.npy"), np.array(cells, dtype=np.int64))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -48,6 +50,7 @@ def test_gloo_world2_shard_and_gather(tmp_path, n_total):
     assert np.array_equal(scores, np.arange(n_total, dtype=np.int32) * 3 + 1)
     assert np.array_equal(ei, (np.arange(n_total) % 7).astype(np.int16))
     assert list(np.load(tmp_path / "t.npy")) == [2.0, 5.0]
+    assert list(np.load(tmp_path / "cells.npy")) == [n_total, 2 * 10 ** 12 + 1]
 
 
 def test_shard_ranges_cover_exactly():
