@@ -329,7 +329,9 @@ def main():
                        "parallelism": f"dp{world}", "kernel": f"sw_{kind}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                         "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                         "traffic": round(traffic["hbm_bytes_per_launch"]) if traffic else None,
+                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/pmc_traffic.json)",
+                         "traffic_detail": traffic, "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
             "valu": {"binding": True, "kernel_gcups": round(kernel_gcups, 1),
                      "ceiling_gcups": round(valu_ceiling, 1),
