@@ -634,9 +634,9 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     uint64_t c = 0;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
         // A short first chunk starts the GPU early; the rest overlap (2-deep).
-        const uint64_t want = (c == 0 && n > chunk) ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8)
-                                                    : chunk;
-        cnt = std::min(want, n - first);
+        const uint64_t this_chunk =
+            (c == 0 && n > chunk) ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8) : chunk;
+        cnt = std::min(this_chunk, n - first);
         // Slots alternate across calls too, so consecutive async calls overlap.
         Slot& s = ctx->slots[ctx->slot_seq++ & 1];
         if (tr.on) tr.submit += tr.lap();
@@ -663,8 +663,8 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
         memcpy(s.h_rlen, b.read_len + first, cnt * sizeof(uint16_t));
         if (gmode) {
             const int64_t* p = b.win_pos + first;
-            const uint16_t* want = b.win_len + first;
-            for (uint64_t i = 0; i < cnt; ++i) s.h_wlen[i] = genome_window(p[i], want[i], b.genome->len);
+            const uint16_t* req = b.win_len + first;
+            for (uint64_t i = 0; i < cnt; ++i) s.h_wlen[i] = genome_window(p[i], req[i], b.genome->len);
             memcpy(s.h_pos, p, cnt * sizeof(int64_t));
         } else {
             memcpy(s.h_wlen, b.win_len + first, cnt * sizeof(uint16_t));
