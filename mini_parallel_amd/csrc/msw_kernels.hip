@@ -543,6 +543,38 @@ __device__ __forceinline__ uint32_t sel_round(const PairMeta& q, uint32_t* strea
 #ifndef MSW_PERM_LEAD_AFF_COORDS
 #define MSW_PERM_LEAD_AFF_COORDS 0
 #endif
+// Wavefront steps per loop iteration, per variant (2 or 4; 4 halves the
+// LDS-address adds and avoids rotating the prefetched window words), and
+// whether an odd KR's last row is folded into the score two steps at a time
+// (one max3 per two steps instead of one max per step).  MI355X, tools/ab_sweep.sh
+// (10k / 65k pairs): 4 steps -- linear 9.00 -> 9.25 / 12.20 -> 12.61 TCUPS,
+// affine 4.97 -> 5.48 / 7.08 -> 7.17; with best-cell keys it loses (linear +
+// coords 6.77 -> 6.03, affine + coords 4.64 -> 3.97 at 10k), so those keep 2.
+#ifndef MSW_STEP_UNROLL_LIN
+#define MSW_STEP_UNROLL_LIN 4
+#endif
+#ifndef MSW_STEP_UNROLL_LIN_COORDS
+#define MSW_STEP_UNROLL_LIN_COORDS 2
+#endif
+#ifndef MSW_STEP_UNROLL_AFF
+#define MSW_STEP_UNROLL_AFF 4
+#endif
+#ifndef MSW_STEP_UNROLL_AFF_COORDS
+#define MSW_STEP_UNROLL_AFF_COORDS 2
+#endif
+#ifndef MSW_FOLD_PAIR
+#define MSW_FOLD_PAIR 1
+#endif
+constexpr int step_unroll(bool affine, bool coords) {
+    return affine ? (coords ? MSW_STEP_UNROLL_AFF_COORDS : MSW_STEP_UNROLL_AFF)
+                  : (coords ? MSW_STEP_UNROLL_LIN_COORDS : MSW_STEP_UNROLL_LIN);
+}
+static_assert(step_unroll(false, false) % 2 == 0 && step_unroll(false, false) <= 4 &&
+                  step_unroll(false, true) % 2 == 0 && step_unroll(false, true) <= 4 &&
+                  step_unroll(true, false) % 2 == 0 && step_unroll(true, false) <= 4 &&
+                  step_unroll(true, true) % 2 == 0 && step_unroll(true, true) <= 4,
+              "steps per iteration are 2 or 4");
+
 constexpr int perm_lead(bool affine, bool coords) {
     return affine ? (coords ? MSW_PERM_LEAD_AFF_COORDS : MSW_PERM_LEAD_AFF)
                   : (coords ? MSW_PERM_LEAD_LIN_COORDS : MSW_PERM_LEAD_LIN);
@@ -565,7 +597,9 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     const PairMeta q = load_meta<SPLIT>(p, g, block, active);
     const int skew = SPLIT ? 2 * (G - 1) + 1 : G - 1;
     // wavefront steps, rounded up to even for the two-step unrolled loop
-    const int steps = (__builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + skew + 1) & ~1;
+    constexpr int kUnroll = step_unroll(AFFINE, COORDS);
+    const int steps =
+        (__builtin_amdgcn_readfirstlane(wave_max_i32(max(q.na, q.nb))) + skew + kUnroll - 1) & ~(kUnroll - 1);
     uint32_t* stream = lds + g * p.lds_stride;
     // Staging.  Read bytes and the first round of window chunks are loaded
     // together (one memory round trip); 16-byte aligned batches under an f16
@@ -657,8 +691,10 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
         // One wavefront step: consumes t1 (this step's diagonal terms), produces
         // t1n (the next step's) from w, the window word of step t + 1.  Called
         // with alternating buffers so the hand-over needs no register copies.
-        auto step = [&](int t, uint32_t w, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR])
+        uint32_t hpend = 0u;  // MSW_FOLD_PAIR: last row's H of the even step, folded with the odd one's
+        auto step = [&](int t, uint32_t w, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR], auto parity)
                         __attribute__((always_inline)) {
+            constexpr int kParity = decltype(parity)::value;
             // Unbiased values cross the lanes (the zero fill is the top boundary),
             // the bias is re-added on arrival: no u16 half ever goes negative.
             // Only H (and affine F) cross: E resp. G of the row above are
@@ -731,33 +767,66 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
                     key_a[r] = max(key_a[r], (h << 16) | nj_a);
                     key_b[r] = max(key_b[r], (h & 0xFFFF0000u) | nj_b);
                 } else {
-                    if (r & 1) best = track_max3(best, hprev, h);
-                    else if (r + 1 == KR) best = F16 ? hmax(best, h) : pk_max(best, h);
+                    if (r & 1) {
+                        best = track_max3(best, hprev, h);
+                    } else if (r + 1 == KR) {
+                        if constexpr (MSW_FOLD_PAIR) {
+                            if constexpr (kParity == 0) hpend = h;
+                            else best = track_max3(best, hpend, h);
+                        } else {
+                            best = F16 ? hmax(best, h) : pk_max(best, h);
+                        }
+                    }
                     hprev = h;
                 }
                 if constexpr (kPermLead > 0) __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (AFFINE) f_bot = up;
         };
-        // Step count rounded up to even: the extra step scores padding columns,
+        // Step count rounded up to a multiple of the steps per iteration: the
+        // extra steps score padding columns,
         // which never reach a real cell's score.
-        // The window words are read from LDS one full iteration (two steps) before
-        // use, so a lone wave never waits on LDS latency.  The read is an asm
+        // The window words are read from LDS two steps or more before use, so
+        // a lone wave never waits on LDS latency.  The read is an asm
         // statement (hipcc would otherwise sink it to the consuming iteration); its
         // wait names the destination, so nothing reads it before the data lands.
-        uint32_t w1 = wp[1], w2 = wp[2];
-        uint2 wn;
-        asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wn) : "v"(lds_wp));
-        for (int t = 0; t < steps; t += 2) {
-            step(t, w1, t1a, t1b);
-            step(t + 1, w2, t1b, t1a);
+        using P0 = std::integral_constant<int, 0>;
+        using P1 = std::integral_constant<int, 1>;
+        if constexpr (kUnroll == 4) {
+            // Four steps per iteration: the words of steps t+1..t+2 (wa) and
+            // t+3..t+4 (wb) are each re-read into the same registers right after
+            // their last use, two steps before they are needed again, and one
+            // address add serves four steps.
+            uint2 wa = make_uint2(wp[1], wp[2]);
+            uint2 wb;
+            asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wb) : "v"(lds_wp));
+            for (int t = 0; t < steps; t += 4) {
+                const uint32_t base = lds_wp + 4u * (uint32_t)t;
+                step(t, wa.x, t1a, t1b, P0{});
+                step(t + 1, wa.y, t1b, t1a, P1{});
+                asm volatile("ds_read2_b32 %0, %1 offset0:5 offset1:6" : "=v"(wa) : "v"(base));
+                asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(wb));
+                step(t + 2, wb.x, t1a, t1b, P0{});
+                step(t + 3, wb.y, t1b, t1a, P1{});
+                asm volatile("ds_read2_b32 %0, %1 offset0:7 offset1:8" : "=v"(wb) : "v"(base));
+                asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(wa));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wb));
+        } else {
+            uint32_t w1 = wp[1], w2 = wp[2];
+            uint2 wn;
+            asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4" : "=v"(wn) : "v"(lds_wp));
+            for (int t = 0; t < steps; t += 2) {
+                step(t, w1, t1a, t1b, P0{});
+                step(t + 1, w2, t1b, t1a, P1{});
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
+                w1 = wn.x;
+                w2 = wn.y;
+                asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4"
+                             : "=v"(wn) : "v"(lds_wp + 4u * (uint32_t)(t + 2)));
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
-            w1 = wn.x;
-            w2 = wn.y;
-            asm volatile("ds_read2_b32 %0, %1 offset0:3 offset1:4"
-                         : "=v"(wn) : "v"(lds_wp + 4u * (uint32_t)(t + 2)));
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wn));
     };
     if (p.trace) t_loop = __builtin_amdgcn_s_memrealtime();
     if (fast) run(std::true_type{});
