@@ -36,12 +36,13 @@ SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 # VALU issue cycles per packed row-step (one wave instruction stream covering
 # 64 lanes x 2 cells = 128 cells) of the f16 fast path at full occupancy: the
 # compiled loop's VALU instructions per row-step (hipcc -S of msw_kernels.hip,
-# KR = 13: linear 124 / 26, +coords 192 / 26, affine 230 / 26, affine+coords
+# KR = 13: linear 243 / 52, +coords 192 / 26, affine 455 / 52, affine+coords
 # 298 / 26) x 4.1 cycles, the issue cost of v_pk_add_f16, v_pk_maximum3_f16,
 # v_perm_b32, v_lshl_or_b32, v_bfi_b32 and v_max3_u32 measured by
 # tools/ubench_valu.hip.  A lone wave issues at most one
 # instruction per ~4.75 cycles, so one-wave-per-SIMD batches sit below this.
-CYCLES_PER_ROW_STEP = {"linear": 19.55, "linear_coords": 30.28, "affine": 36.27,
+# (score-only loops run 4 steps per iteration, best-cell loops 2).
+CYCLES_PER_ROW_STEP = {"linear": 19.16, "linear_coords": 30.28, "affine": 35.88,
                        "affine_coords": 46.99}
 
 
