@@ -98,9 +98,13 @@ def test_files_mode_compat(tmp_path, oracle):
 
 
 @pytest.mark.gpu
-def test_full_wgs_sw_and_resume(tmp_path, oracle):
+@pytest.mark.parametrize("bgzf", [False, True])
+def test_full_wgs_sw_and_resume(tmp_path, oracle, bgzf):
+    """--full-wgs --score-mode sw over gzip or BGZF lane files (BGZF: libdeflate
+    block inflate, several threads per file): per-file i64 sums equal the
+    oracle's, checkpoint/resume skips finished files."""
     from mini_parallel_amd.synthetic import write_wgs_dataset
-    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=2, reads_per_lane=2, reads_per_file=1500)
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=2, reads_per_lane=2, reads_per_file=1500, bgzf=bgzf)
     env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "2",
            "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "700", "WGS_RUN_ID": "t1"}
     args = ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
