@@ -86,3 +86,33 @@ def test_pack_batch():
     assert R.shape == (2, 16) and W.shape == (2, 48)
     assert list(rl) == [4, 0] and list(wl) == [8, 40]
     assert bytes(R[0, :4]) == b"ACGT" and not R[1].any()
+
+
+def _build_c_consumer(tmp_path):
+    """Compile tests/c/abi_c99.c as strict C99 against include/ and link it to
+    libmsw.so (the header must be plain C; every entry point must link)."""
+    exe = str(tmp_path / "abi_c99")
+    src = os.path.join(ROOT, "tests", "c", "abi_c99.c")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-pedantic", "-Wall", "-Wextra", "-Werror", "-I",
+                    os.path.join(ROOT, "include"), src, "-o", exe, "-L", libdir, "-lmsw",
+                    "-Wl,-rpath," + libdir], check=True)
+    return exe
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present (the gpu variant runs there)")
+def test_c99_consumer_no_gpu(tmp_path):
+    r = subprocess.run([_build_c_consumer(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "abi_c99 ok (no gpu)" in r.stdout
+
+
+@pytest.mark.gpu
+def test_c99_consumer_gpu():
+    """The prebuilt C99 consumer (__graft_entry__.build()) scores a known-answer
+    pair through the C ABI on the GPU."""
+    exe = os.path.join(ROOT, "tests", "c", "abi_c99")
+    assert os.path.exists(exe), "tests/c/abi_c99 not built: run __graft_entry__.build()"
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "abi_c99 ok (gpu)" in r.stdout
