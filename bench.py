@@ -126,6 +126,40 @@ def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j):
     return cpu, parity
 
 
+def cut_roofline(ctx, dev, stream):
+    """The path's HBM-bound kernel on its own: msw_genome_cut_device cutting
+    1M 300 bp windows (random positions in a 64 Mbp genome) into a 304 B/row
+    slab, timed with HIP events on the launch stream.  Algorithmic bytes per
+    window: 300 genome + 304 slab + 8 position + 2 requested + 2 clipped length."""
+    import torch
+    n, ws, glen, reps = 1_000_000, 304, 64 << 20, 20
+    rng = np.random.default_rng(7)
+    genome = ctx.load_genome(rng.choice(np.frombuffer(b"ACGT", np.uint8), glen))
+    d_pos = torch.from_numpy(rng.integers(0, glen - 300, n).astype(np.int64)).to(dev)
+    d_want = torch.full((n,), 300, dtype=torch.int16, device=dev)
+    d_wins = torch.empty((n, ws), dtype=torch.uint8, device=dev)
+    d_len = torch.empty(n, dtype=torch.int16, device=dev)
+
+    def launch():
+        genome.cut_device(d_pos.data_ptr(), d_want.data_ptr(), n, d_wins.data_ptr(), ws, d_len.data_ptr(),
+                          stream.cuda_stream)
+    for _ in range(3):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    t = e0.elapsed_time(e1) * 1e-3 / reps
+    genome.close()
+    alg = n * (300 + ws + 8 + 2 + 2)
+    return {"kernel": "cut_windows_kernel", "bound": "hbm", "achieved": round(alg / t / 1e9, 1),
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "avg_launch_ms": round(t * 1e3, 4), "alg_bytes_per_launch": alg,
+            "workload": "1M x 300 bp windows from a 64 Mbp HBM-resident genome -> 304 B/row slab"}
+
+
 def pcie_rates(ctx, batch, scoring, cells, gpu_scores):
     from mini_parallel_amd.aligner import pinned_empty
 
@@ -307,6 +341,7 @@ def main():
         pcie = None
         if not args.no_pcie:
             pcie = pcie_rates(ctx, batch, scoring, cells, gpu_scores)
+            cut = cut_roofline(ctx, dev, stream)
 
         line = {
             "metric": "GCUPS (billion cell updates/s) on 150bp reads, 1/2/4/8 MI355X; bit-exact scores",
@@ -344,6 +379,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "pcie_inclusive": pcie,
+            "cut_windows_roofline": cut if not args.no_pcie else None,
             "gathered_scores": gathered,
         }
         print(json.dumps(line), flush=True)

@@ -166,6 +166,15 @@ int msw_genome_create(msw_ctx* ctx, const uint8_t* seq, uint64_t len, msw_genome
 void msw_genome_destroy(msw_genome* g);
 uint64_t msw_genome_length(const msw_genome* g);
 
+/* Device-resident form: cut the windows of n (position, requested length)
+ * pairs (device arrays) into a device slab wins[n][win_stride] (win_stride a
+ * multiple of 16, wins 16-byte aligned; zero-padded), writing the clipped
+ * lengths to win_len_out (may be NULL) -- the input msw_align_batch_device /
+ * msw_align_batch_planned take.  Enqueued on `stream` (NULL = the context's
+ * compute stream).  Windows are also clipped at win_stride. */
+int msw_genome_cut_device(msw_ctx* ctx, const msw_genome* g, const int64_t* win_pos, const uint16_t* win_len,
+                          uint64_t n, uint8_t* wins, uint32_t win_stride, uint16_t* win_len_out, void* stream);
+
 /* Reads against genome windows: pair p scores reads[p*read_stride ..][0,
  * read_len[p]) against genome[win_pos[p], win_pos[p] + win_len[p]), the
  * window clipped at the genome end; win_pos < 0 or >= the genome length is an

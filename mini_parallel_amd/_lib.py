@@ -28,7 +28,7 @@ EXPORTED = (
     "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
     "msw_plan_create", "msw_align_batch_planned", "msw_plan_destroy",
     "msw_genome_create", "msw_genome_destroy", "msw_genome_length", "msw_align_reads",
-    "msw_align_reads_async",
+    "msw_align_reads_async", "msw_genome_cut_device",
 )
 # include/msw_fastq.h
 FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_stats",
@@ -98,6 +98,7 @@ def _declare(L):
         "msw_genome_create": (I, [P, P, ctypes.c_uint64, ctypes.POINTER(P)]),
         "msw_genome_destroy": (None, [P]),
         "msw_genome_length": (ctypes.c_uint64, [P]),
+        "msw_genome_cut_device": (I, [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P, P]),
         "msw_align_reads": (I, [P, ctypes.POINTER(ScoringT), P, ctypes.POINTER(ReadBatchT),
                                 ctypes.POINTER(OutT), ctypes.c_uint64]),
         "msw_align_reads_async": (I, [P, ctypes.POINTER(ScoringT), P, ctypes.POINTER(ReadBatchT),

@@ -330,6 +330,16 @@ class Genome:
     def __len__(self) -> int:
         return int(lib().msw_genome_length(self.handle))
 
+    def cut_device(self, pos_ptr: int, win_len_ptr: int, n: int, wins_ptr: int, win_stride: int,
+                   win_len_out_ptr: int = 0, stream: int = 0) -> None:
+        """msw_genome_cut_device: cut n windows (device arrays of positions and
+        requested lengths) into a device slab, clipped lengths to
+        win_len_out; enqueued on ``stream`` (0 = the context's stream)."""
+        check(lib().msw_genome_cut_device(self.ctx.handle, self.handle, ctypes.c_void_p(pos_ptr),
+                                          ctypes.c_void_p(win_len_ptr), n, ctypes.c_void_p(wins_ptr),
+                                          win_stride, ctypes.c_void_p(win_len_out_ptr or None),
+                                          ctypes.c_void_p(stream or None)))
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:
             lib().msw_genome_destroy(self._h)

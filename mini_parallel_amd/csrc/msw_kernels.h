@@ -118,12 +118,13 @@ hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_r
 hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, bool coords,
                            hipStream_t stream);
 
-// Genome-resident windows: out[p * ws ..] = genome[pos[p], pos[p] + wlen[p]),
-// zero-padded; ws % 16 == 0, wlen already clipped to the genome, genome
-// allocation padded by >= 20 bytes past its end.
+// Genome-resident windows: out[p * ws ..] = genome[pos[p], pos[p] + len),
+// len = want[p] clipped to the genome (0 outside it), zero-padded to ws;
+// out_len[p] = len when out_len != nullptr.  ws % 16 == 0, genome allocation
+// padded by >= 20 bytes past its end.
 constexpr uint32_t kGenomePad = 64;
-hipError_t launch_cut_windows(const uint8_t* genome, const int64_t* pos, const uint16_t* wlen, uint8_t* out,
-                              uint32_t ws, uint64_t n, hipStream_t stream);
+hipError_t launch_cut_windows(const uint8_t* genome, uint64_t glen, const int64_t* pos, const uint16_t* want,
+                              uint8_t* out, uint16_t* out_len, uint32_t ws, uint64_t n, hipStream_t stream);
 
 // smith_waterman_align restated: result must be zeroed before the launch.
 hipError_t launch_compat(const uint8_t* s1, const uint8_t* s2, int32_t* result, uint64_t L,

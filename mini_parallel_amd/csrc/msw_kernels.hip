@@ -981,26 +981,32 @@ __global__ __launch_bounds__(256) void sw_compat_kernel(const uint8_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-// Window cut for genome-resident batches (msw_align_reads): pair p's window
-// genome[pos[p], pos[p] + wlen[p]) -> out[p * ws ..], zero-padded to ws.  One
-// thread per 16-byte output chunk: five aligned dword loads, v_alignbyte to
-// the window's byte offset, one 16-byte store (consecutive threads write
-// consecutive chunks of a row).  The host clips wlen to the genome and pads
-// the genome allocation by >= 20 bytes, so the fifth dword never leaves it.
+// Window cut for genome-resident batches (msw_align_reads,
+// msw_genome_cut_device): pair p's window genome[pos[p], pos[p] + len) with
+// len = want[p] clipped at the genome end (0 outside it) and at ws -> out[p * ws ..],
+// zero-padded to ws; out_len[p] = len when out_len is given.  One thread per
+// 16-byte output chunk: five aligned dword loads, v_alignbyte to the window's
+// byte offset, one 16-byte store (consecutive threads write consecutive
+// chunks of a row).  The genome allocation is padded by >= 20 bytes, so the
+// fifth dword never leaves it.  HBM-bound: ~2 bytes moved per window byte.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void cut_windows_kernel(const uint8_t* __restrict__ g,
+__global__ __launch_bounds__(256) void cut_windows_kernel(const uint8_t* __restrict__ g, uint64_t glen,
                                                           const int64_t* __restrict__ pos,
-                                                          const uint16_t* __restrict__ wlen,
-                                                          uint8_t* __restrict__ out, uint32_t chunks,
-                                                          uint64_t ws, uint64_t n) {
+                                                          const uint16_t* __restrict__ want,
+                                                          uint8_t* __restrict__ out, uint16_t* __restrict__ out_len,
+                                                          uint32_t chunks, uint64_t ws, uint64_t n) {
     const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     const uint64_t p = t / chunks;
     if (p >= n) return;
     const uint32_t c = (uint32_t)(t - p * chunks);
-    const int rem = (int)wlen[p] - 16 * (int)c;
+    const uint64_t start = (uint64_t)pos[p];  // negative positions wrap past glen
+    const uint64_t room = start < glen ? glen - start : 0;
+    const int len = (int)min(min((uint64_t)want[p], room), ws);
+    if (out_len && c == 0) out_len[p] = (uint16_t)len;
+    const int rem = len - 16 * (int)c;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     if (rem > 0) {
-        const uint64_t a = (uint64_t)pos[p] + 16u * c;
+        const uint64_t a = start + 16u * c;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(g + (a & ~3ull));
         uint32_t x[5];
 #pragma unroll
@@ -1123,15 +1129,15 @@ hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, 
     return hipGetLastError();
 }
 
-hipError_t launch_cut_windows(const uint8_t* genome, const int64_t* pos, const uint16_t* wlen, uint8_t* out,
-                              uint32_t ws, uint64_t n, hipStream_t stream) {
+hipError_t launch_cut_windows(const uint8_t* genome, uint64_t glen, const int64_t* pos, const uint16_t* want,
+                              uint8_t* out, uint16_t* out_len, uint32_t ws, uint64_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if (ws == 0 || ws % 16 != 0 || ((uintptr_t)out & 15) != 0) return hipErrorInvalidValue;
     const uint32_t chunks = ws / 16;
     const uint64_t blocks = (n * chunks + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(cut_windows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, genome, pos, wlen, out,
-                       chunks, (uint64_t)ws, n);
+    hipLaunchKernelGGL(cut_windows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, genome, glen, pos, want, out,
+                       out_len, chunks, (uint64_t)ws, n);
     return hipGetLastError();
 }
 

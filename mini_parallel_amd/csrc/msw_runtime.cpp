@@ -695,7 +695,8 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
         // the compute stream, results back on the d2h stream -- chunk k+1's
         // uploads and chunk k-1's readback overlap chunk k's kernel.
         if (gmode)
-            HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, s.d_pos, s.d_wlen, s.d_wins, ws, cnt, up));
+            HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, b.genome->len, s.d_pos, s.d_wlen, s.d_wins, nullptr, ws,
+                                            cnt, up));
         if (multi_chunk) {
             HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
             HIP_TRY(hipStreamWaitEvent(ctx->compute, s.uploaded, 0));
@@ -1129,6 +1130,21 @@ void msw_genome_destroy(msw_genome* g) {
 }
 
 uint64_t msw_genome_length(const msw_genome* g) { return g ? g->len : 0; }
+
+int msw_genome_cut_device(msw_ctx* ctx, const msw_genome* g, const int64_t* win_pos, const uint16_t* win_len,
+                          uint64_t n, uint8_t* wins, uint32_t win_stride, uint16_t* win_len_out, void* stream) {
+    if (!ctx || !g) return fail(MSW_E_INVALID, "ctx/genome is NULL");
+    if (g->ctx != ctx) return fail(MSW_E_INVALID, "genome belongs to another context");
+    if (n == 0) return MSW_OK;
+    if (!win_pos || !win_len || !wins) return fail(MSW_E_INVALID, "NULL array");
+    if (win_stride == 0 || win_stride % 16 != 0 || ((uintptr_t)wins & 15) != 0)
+        return fail(MSW_E_INVALID, "win_stride must be a non-zero multiple of 16 and wins 16-byte aligned");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    HIP_TRY(msw::launch_cut_windows(g->d_seq, g->len, win_pos, win_len, wins, win_len_out, win_stride, n, st));
+    return MSW_OK;
+}
 
 int msw_align_reads(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g, const msw_read_batch_t* batch,
                     msw_out_t* out, uint64_t chunk_pairs) {

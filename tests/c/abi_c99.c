@@ -27,7 +27,7 @@ int main(int argc, char** argv) {
                    (fn_t)msw_align_batch_planned, (fn_t)msw_plan_destroy, (fn_t)msw_align_compat,
                    (fn_t)msw_host_alloc, (fn_t)msw_host_free, (fn_t)msw_genome_create,
                    (fn_t)msw_genome_destroy, (fn_t)msw_genome_length, (fn_t)msw_align_reads,
-                   (fn_t)msw_align_reads_async, (fn_t)msw_dev_alloc, (fn_t)msw_dev_free,
+                   (fn_t)msw_align_reads_async, (fn_t)msw_genome_cut_device, (fn_t)msw_dev_alloc, (fn_t)msw_dev_free,
                    (fn_t)msw_memcpy_h2d, (fn_t)msw_memcpy_d2h, (fn_t)msw_synchronize,
                    (fn_t)msw_last_error, (fn_t)msw_version, (fn_t)msw_fastq_open,
                    (fn_t)msw_fastq_close, (fn_t)msw_fastq_next, (fn_t)msw_fastq_stats,

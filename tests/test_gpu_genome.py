@@ -217,3 +217,37 @@ def test_async_calls_in_flight(gpu_ctx, oracle):
     for p, r in zip(parts, got[:3]):
         assert_same(r, tuple(e[p] for e in expect), True)
     assert_same(got[3], expect, True)
+
+
+def test_genome_cut_device_matches_host_cut(gpu_ctx, oracle):
+    """msw_genome_cut_device on device arrays: the same windows and clipped
+    lengths as the host restatement, then scored through the device API."""
+    import torch
+    g, R, rl, pos, want = genome_case(5000, 700_001, seed=71)
+    want[20] = 400  # clipped at the slab stride (320)
+    genome = gpu_ctx.load_genome(g)
+    dev = torch.device("cuda", 0)
+    ws = 320
+    d_pos = torch.from_numpy(pos).to(dev)
+    d_want = torch.from_numpy(want.view(np.int16)).to(dev)
+    d_wins = torch.full((pos.size, ws), 0xAB, dtype=torch.uint8, device=dev)
+    d_len = torch.zeros(pos.size, dtype=torch.int16, device=dev)
+    genome.cut_device(d_pos.data_ptr(), d_want.data_ptr(), pos.size, d_wins.data_ptr(), ws, d_len.data_ptr())
+    torch.cuda.synchronize()
+    W, wl = host_windows(g, pos, np.minimum(want, ws).astype(np.uint16))
+    got_len = d_len.cpu().numpy().view(np.uint16)
+    assert np.array_equal(got_len, wl)
+    got = d_wins.cpu().numpy()
+    assert np.array_equal(got[:, :W.shape[1]], W) and not got[:, W.shape[1]:].any()
+    sc = Scoring(want_coords=True)
+    d_reads = torch.from_numpy(R).to(dev)
+    d_rl = torch.from_numpy(rl.view(np.int16)).to(dev)
+    score = torch.zeros(pos.size, dtype=torch.int32, device=dev)
+    ei = torch.zeros(pos.size, dtype=torch.int16, device=dev)
+    ej = torch.zeros(pos.size, dtype=torch.int16, device=dev)
+    gpu_ctx.align_batch_device(d_reads.data_ptr(), d_rl.data_ptr(), d_wins.data_ptr(), d_len.data_ptr(),
+                               R.shape[1], ws, pos.size, score.data_ptr(), int(rl.max()), ws, sc,
+                               ei.data_ptr(), ej.data_ptr())
+    gpu_ctx.synchronize()
+    assert_same((score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy()),
+                oracle_run(oracle, R, rl, W, wl, sc), True)
