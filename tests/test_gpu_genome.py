@@ -251,3 +251,23 @@ def test_genome_cut_device_matches_host_cut(gpu_ctx, oracle):
     gpu_ctx.synchronize()
     assert_same((score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy()),
                 oracle_run(oracle, R, rl, W, wl, sc), True)
+
+
+def test_error_paths(gpu_ctx):
+    """Range / argument errors of the new entry points fail loudly, before any
+    launch, with a message (the Err(String) analogue)."""
+    import ctypes
+    from mini_parallel_amd._lib import lib
+    g = gpu_ctx.load_genome(b"ACGT" * 100)
+    R = np.zeros((2, 16), np.uint8)
+    with pytest.raises(mpa.MswError, match="window length"):  # requested window > 4096
+        gpu_ctx.align_reads(g, R, np.array([4, 4], np.uint16), np.zeros(2, np.int64),
+                            np.array([4097, 4], np.uint16))
+    with pytest.raises(mpa.MswError, match="unknown ticket"):
+        from mini_parallel_amd._lib import check
+        check(lib().msw_wait(gpu_ctx.handle, ctypes.c_uint64(10 ** 12)))
+    with pytest.raises(mpa.MswError, match="multiple of 16"):
+        g.cut_device(0, 0, 1, 0, 30)
+    p = gpu_ctx.align_reads(g, R, np.array([4, 4], np.uint16), np.zeros(2, np.int64),
+                            np.array([4, 4], np.uint16), asynchronous=True)
+    assert list(p.wait()[0]) == [0, 0]  # zero reads vs ACGT: nothing matches byte 0
