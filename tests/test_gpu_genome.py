@@ -266,8 +266,10 @@ def test_error_paths(gpu_ctx):
     with pytest.raises(mpa.MswError, match="unknown ticket"):
         from mini_parallel_amd._lib import check
         check(lib().msw_wait(gpu_ctx.handle, ctypes.c_uint64(10 ** 12)))
-    with pytest.raises(mpa.MswError, match="multiple of 16"):
-        g.cut_device(0, 0, 1, 0, 30)
+    with pytest.raises(mpa.MswError, match="NULL array"):
+        g.cut_device(0, 0, 1, 0, 32)
+    with pytest.raises(mpa.MswError, match="multiple of 16"):  # validated before anything is touched
+        g.cut_device(16, 16, 1, 16, 30)
     p = gpu_ctx.align_reads(g, R, np.array([4, 4], np.uint16), np.zeros(2, np.int64),
                             np.array([4, 4], np.uint16), asynchronous=True)
     assert list(p.wait()[0]) == [0, 0]  # zero reads vs ACGT: nothing matches byte 0
