@@ -412,6 +412,22 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
         const int nb = (wlen[i] + 15) / 16;
         return kr * 257 + nb;
     };
+    // One key (fixed-length reads and windows, the common case): one bucket in
+    // input order, no sort.
+    int kmin = kKeys, kmax = -1;
+    uint32_t gm = 0, gn = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int k = key_of(i);
+        kmin = std::min(kmin, k);
+        kmax = std::max(kmax, k);
+        gm = std::max<uint32_t>(gm, rlen[i]);
+        gn = std::max<uint32_t>(gn, wlen[i]);
+    }
+    if (n && kmin == kmax) {
+        for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+        buckets.push_back({0, (uint32_t)n, gm, gn});
+        return;
+    }
     for (uint64_t i = 0; i < n; ++i) hist[key_of(i) + 1]++;
     for (int k = 0; k < kKeys; ++k) hist[k + 1] += hist[k];
     std::vector<uint32_t> pos(hist.begin(), hist.end() - 1);
