@@ -34,6 +34,8 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <fcntl.h>
+#include <unistd.h>
 #include <ctime>
 #include <vector>
 
@@ -91,7 +93,7 @@ struct Args {
     std::string seq1, seq2;
     bool has_seq1 = false, has_seq2 = false, files = false, gpu = false, test_wgs = false, full_wgs = false;
     long chunk_size = 1, num_files = -1;
-    std::string score_mode = "compat", gap_model = "linear", reference, checkpoint_dir = ".", json;
+    std::string score_mode = "compat", gap_model = "linear", reference, checkpoint_dir = ".", json, scores_out;
     int match = 2, mismatch = -1, gap_open = 3, gap_extend = -1, window = 0, num_gpus = 1;
 };
 
@@ -115,6 +117,8 @@ void usage() {
         "      --window N               window length (default 2 x read length)\n"
         "      --num-gpus N             GPUs for --full-wgs\n"
         "      --checkpoint-dir DIR     where checkpoint_<run_id>.json lives (default .)\n"
+        "      --scores-out DIR         --full-wgs sw: per-read results, one <lane file>.scores per file\n"
+        "                               (8 bytes per read in file order: i32 score, i16 end_i, i16 end_j)\n"
         "      --json PATH              write a JSON run record\n"
         "  -h, --help\n");
 }
@@ -150,6 +154,7 @@ Args parse_args(int argc, char** argv) {
         else if (s == "--num-gpus") a.num_gpus = atoi(v().c_str());
         else if (s == "--checkpoint-dir") a.checkpoint_dir = v();
         else if (s == "--json") a.json = v();
+        else if (s == "--scores-out") a.scores_out = v();
         else if (s == "-h" || s == "--help") { usage(); exit(0); }
         else die("error: unexpected argument '" + s + "' found\n\nFor more information, try '--help'.");
     }
@@ -415,6 +420,7 @@ struct Chunk {
     SlabPool* pool = nullptr;
     SlabPool::Slab* slab = nullptr;  // reads n x kReadStride, rlen, pos
     uint64_t n = 0;
+    uint64_t first_read = 0;         // index of the chunk's first read in its file
     bool last = false;               // last chunk of its file
     const uint8_t* reads() const { return slab->reads; }
     const uint16_t* rlen() const { return slab->rlen; }
@@ -430,6 +436,7 @@ struct FileState {
     std::atomic<unsigned long long> bases{0}, reads{0};
     std::atomic<int> outstanding{0};
     std::atomic<bool> reader_done{false}, failed{false}, finished{false};
+    int scores_fd = -1;  // --scores-out: per-read records, written at the read's offset
     Clock::time_point t0;
     double ms = 0;
     std::string error;
@@ -508,6 +515,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         FileState& f = *st[fi];
         if (f.finished.exchange(true)) return;  // exactly once (reader or GPU thread)
         f.ms = ms_since(f.t0);
+        if (f.scores_fd >= 0) {
+            close(f.scores_fd);
+            f.scores_fd = -1;
+        }
         FileCheckpoint c;
         c.file_path = f.path;
         c.file_index = fi;
@@ -549,6 +560,13 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 const size_t fi = todo[k];
                 FileState& f = *st[fi];
                 f.t0 = Clock::now();
+                if (sw && !a.scores_out.empty()) {
+                    const size_t slash = f.path.find_last_of('/');
+                    const std::string out = a.scores_out + "/" +
+                                            (slash == std::string::npos ? f.path : f.path.substr(slash + 1)) + ".scores";
+                    f.scores_fd = open(out.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+                    if (f.scores_fd < 0) die("error: cannot create " + out);
+                }
                 printf("  Processing file %zu/%zu: %s\n", fi + 1, files.size(), f.path.c_str());
                 fflush(stdout);
                 msw_fastq* fq = nullptr;
@@ -559,9 +577,11 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     if (f.outstanding.load() == 0) finish_file(fi);
                     continue;
                 }
+                uint64_t reads_so_far = 0;
                 for (;;) {
                     std::unique_ptr<Chunk> c(new Chunk());
                     c->file_index = fi;
+                    c->first_read = reads_so_far;
                     c->pool = &slabs;
                     c->slab = slabs.get();
                     if (msw_fastq_next(fq, c->slab->reads, c->slab->rlen, kReadStride, chunk, &c->n,
@@ -572,6 +592,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         break;
                     }
                     if (c->n == 0) break;
+                    reads_so_far += c->n;
                     f.outstanding.fetch_add(1);
                     queue.push(std::move(c));
                 }
@@ -617,6 +638,21 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 } else {
                     for (uint64_t i = 0; i < fl.c->n; ++i) chunk_score += fl.score[i];
                     cells += fl.cells;
+                    if (f.scores_fd >= 0) {
+                        // chunks of one file may finish on different GPUs in any
+                        // order: each lands at its reads' own offset
+                        std::vector<uint8_t> rec(fl.c->n * 8);
+                        for (uint64_t i = 0; i < fl.c->n; ++i) {
+                            memcpy(&rec[i * 8], &fl.score[i], 4);
+                            memcpy(&rec[i * 8 + 4], &fl.ei[i], 2);
+                            memcpy(&rec[i * 8 + 6], &fl.ej[i], 2);
+                        }
+                        if (pwrite(f.scores_fd, rec.data(), rec.size(), (off_t)(fl.c->first_read * 8)) !=
+                            (ssize_t)rec.size()) {
+                            fprintf(stderr, "  error writing scores for %s\n", f.path.c_str());
+                            f.failed = true;
+                        }
+                    }
                 }
                 f.score += chunk_score;
                 f.bases += fl.bases;

@@ -107,16 +107,22 @@ def test_full_wgs_sw_and_resume(tmp_path, oracle, bgzf):
     ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=2, reads_per_lane=2, reads_per_file=1500, bgzf=bgzf)
     env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "2",
            "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "700", "WGS_RUN_ID": "t1"}
+    (tmp_path / "scores").mkdir()
     args = ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
-            "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json")]
+            "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json"),
+            "--scores-out", str(tmp_path / "scores")]
     r = run(args, env=env, cwd=tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr
     want = 0
     per_file = []
-    for b in ds["batches"]:
-        s, _, _ = oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=8)
+    rec_t = np.dtype([("score", "<i4"), ("end_i", "<i2"), ("end_j", "<i2")])
+    for f, b in zip(ds["files"], ds["batches"]):
+        s, i, j = oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=8)
         per_file.append(int(s.astype(np.int64).sum()))
         want += per_file[-1]
+        # per-read results, in file order (chunks land at their own offsets)
+        got = np.fromfile(tmp_path / "scores" / (os.path.basename(f) + ".scores"), dtype=rec_t)
+        assert np.array_equal(got["score"], s) and np.array_equal(got["end_i"], i) and np.array_equal(got["end_j"], j)
     rec = json.load(open(tmp_path / "rec.json"))
     assert rec["total_score"] == want and rec["total_reads"] == 6000
     # the reference's BenchmarkResult fields (tools/benchmark.rs:17-34) + GCUPS
