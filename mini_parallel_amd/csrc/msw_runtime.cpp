@@ -1180,7 +1180,8 @@ int msw_align_reads_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genom
 
 void* msw_host_alloc(size_t bytes) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    // portable: the --full-wgs readers fill slabs that any GPU's context DMAs
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
         fail(MSW_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
         return nullptr;
     }
