@@ -194,20 +194,20 @@ def pcie_rates(ctx, batch, scoring, cells, gpu_scores):
             out[key] = {"gcups": round(cells / best / 1e9, 2), "ms_per_batch": round(best * 1e3, 3)}
             if best_v is None or out[key]["gcups"] > out[best_v]["gcups"]:
                 best_v = key
-    # Streaming: a run of batches submitted asynchronously, two in flight
-    # (msw_align_reads_async + wait on the previous ticket), as the --full-wgs
+    # Streaming: a run of batches submitted asynchronously, three in flight
+    # (msw_align_reads_async + wait on the oldest ticket), as the --full-wgs
     # driver feeds chunks: the steady-state host-to-host rate.
-    reps = 16
+    reps, depth = 24, 3
     arrs = variants["genome_pinned"][1]
     for _ in range(2):
         ts = time.perf_counter()
-        prev = None
+        pend = []
         for _ in range(reps):
-            cur = ctx.align_reads(genome, *arrs, scoring=scoring, asynchronous=True)
-            if prev is not None:
-                prev.wait()
-            prev = cur
-        s_last = prev.wait()[0]
+            pend.append(ctx.align_reads(genome, *arrs, scoring=scoring, asynchronous=True))
+            if len(pend) == depth:
+                pend.pop(0).wait()
+        while pend:
+            s_last = pend.pop(0).wait()[0]
         dt = (time.perf_counter() - ts) / reps
     if not np.array_equal(s_last, gpu_scores):
         raise SystemExit("pcie streaming variant disagrees with the device-resident scores")

@@ -94,8 +94,9 @@ typedef struct msw_ctx msw_ctx;
 int msw_device_count(int* n);
 int msw_device_info(int ordinal, msw_device_info_t* out);
 
-/* gpu.rs:97-132 get_opencl_context/init_opencl: one context per device with a
- * compute stream, a copy stream and double-buffered pinned staging. */
+/* gpu.rs:97-132 get_opencl_context/init_opencl: one context per device with
+ * compute, copy and readback streams and three pinned staging slots (up to
+ * three chunks in flight). */
 int msw_ctx_create(int ordinal, msw_ctx** out);
 void msw_ctx_destroy(msw_ctx* ctx);
 

@@ -615,8 +615,9 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
             msw_genome* gen = nullptr;
             if (sw && msw_genome_create(ctx.h, (const uint8_t*)genome.data(), genome.size(), &gen) != MSW_OK)
                 die(std::string("GPU genome upload error: ") + msw_last_error());
-            // One chunk in flight while the next is staged (msw_align_reads_async
-            // + msw_wait on the previous ticket).
+            // Up to three chunks in flight (msw_align_reads_async; msw_wait on the
+            // oldest ticket before a fourth is staged): the context's three
+            // staging slots keep uploads of chunk k+1 under kernel k.
             struct InFlight {
                 std::unique_ptr<Chunk> c;
                 std::vector<uint16_t> want;
@@ -660,7 +661,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 if (f.outstanding.fetch_sub(1) == 1 && f.reader_done.load()) finish_file(fl.c->file_index);
                 fl.c.reset();
             };
-            std::unique_ptr<InFlight> prev;
+            std::deque<std::unique_ptr<InFlight>> pending;
+            constexpr size_t kDepth = 3;
             for (;;) {
                 std::unique_ptr<Chunk> c = queue.pop();
                 if (!c) break;
@@ -690,8 +692,11 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         fprintf(stderr, "  GPU %d alignment error: %s\n", g, msw_last_error());
                         fl->failed = true;
                     }
-                    if (prev) settle(*prev);
-                    prev = std::move(fl);
+                    pending.push_back(std::move(fl));
+                    if (pending.size() >= kDepth) {
+                        settle(*pending.front());
+                        pending.pop_front();
+                    }
                 } else {
                     // compat: chunk concat self-aligned (aligner.rs:269-276, :365-373)
                     long long chunk_score = 0;
@@ -714,7 +719,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     if (f.outstanding.fetch_sub(1) == 1 && f.reader_done.load()) finish_file(c->file_index);
                 }
             }
-            if (prev) settle(*prev);
+            while (!pending.empty()) {
+                settle(*pending.front());
+                pending.pop_front();
+            }
             msw_genome_destroy(gen);
         });
     }

@@ -207,9 +207,13 @@ struct msw_ctx {
     int device = 0;
     int cu_count = 256;
     hipStream_t compute = nullptr, copy = nullptr, d2h = nullptr;
-    Slot slots[2];
+    // Staging slots, used round robin by successive chunks (and calls): with
+    // three, the host stages chunk k+1 while k runs and k-1 drains, so the
+    // uploads of k+1 finish under kernel k.
+    static constexpr int kSlots = 3;
+    Slot slots[kSlots];
     uint64_t next_ticket = 1, done_ticket = 0;
-    uint64_t slot_seq = 0;  // chunks submitted (slot = slot_seq & 1)
+    uint64_t slot_seq = 0;  // chunks submitted (slot = slot_seq % kSlots)
     // compat buffers
     uint8_t *c_s1 = nullptr, *c_s2 = nullptr;
     int32_t* c_res = nullptr;
@@ -654,7 +658,7 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
             (c == 0 && n > chunk) ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8) : chunk;
         cnt = std::min(this_chunk, n - first);
         // Slots alternate across calls too, so consecutive async calls overlap.
-        Slot& s = ctx->slots[ctx->slot_seq++ & 1];
+        Slot& s = ctx->slots[ctx->slot_seq++ % msw_ctx::kSlots];
         if (tr.on) tr.submit += tr.lap();
         if ((rc = drain_slot(s))) return rc;  // the slot's previous chunk must be out before reuse
         if (tr.on) tr.wait += tr.lap();
@@ -740,7 +744,8 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     }
     if (sync) {
         if (tr.on) tr.submit += tr.lap();
-        if ((rc = drain_slot(ctx->slots[0])) || (rc = drain_slot(ctx->slots[1]))) return rc;
+        for (Slot& sl : ctx->slots)
+            if ((rc = drain_slot(sl))) return rc;
         if (tr.on) tr.wait += tr.lap();
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
