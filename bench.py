@@ -14,8 +14,9 @@ as north_star prescribes).  value = cells of all ranks / max-over-ranks time.
 Extra fields: ``roofline`` (HBM, as north_star asks; algorithmic bytes per
 launch / average launch time from HIP events on the launch stream), ``valu``
 (the binding VALU-integer ceiling), ``cpu_baseline`` (the C oracle on the
-host cores, bounded sample, rank 0 only) and ``parity`` (GPU vs oracle on
-that sample).
+host cores, bounded sample, rank 0 at N = 1 only), ``parity`` (GPU vs oracle
+on that sample; at N > 1 rank 0's first 4096 pairs, untimed) and, at N = 1,
+``pcie_inclusive`` / ``cut_windows_roofline``.
 """
 from __future__ import annotations
 
@@ -124,6 +125,23 @@ def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j):
         mism += int(((si != gpu_i[:n1]) | (sj != gpu_j[:n1])).sum())
     parity = {"checked_pairs": ns, "checked_pairs_scalar": n1, "mismatches": mism, "bit_exact": mism == 0}
     return cpu, parity
+
+
+def parity_sample(batch, scoring, gpu_scores, gpu_i, gpu_j, n=4096):
+    """Parity only (N > 1: the CPU baseline is timed at N = 1 alone): rank 0's
+    first n pairs against the SIMD restatement, untimed."""
+    from oracle import oracle_lib
+    oracle_lib.build()
+    n = min(n, batch.n_pairs)
+    cs, ci, cj, _ = oracle_lib.sw_batch_simd(batch.reads[:n], batch.read_len[:n], batch.wins[:n],
+                                             batch.win_len[:n], threads=min(16, os.cpu_count() or 1),
+                                             coords=scoring.want_coords, match=scoring.match,
+                                             mismatch=scoring.mismatch, gap_open=scoring.gap_open,
+                                             gap_extend=scoring.gap_extend, affine=scoring.affine)
+    mism = int((cs != gpu_scores[:n]).sum())
+    if scoring.want_coords:
+        mism += int(((ci != gpu_i[:n]) | (cj != gpu_j[:n])).sum())
+    return {"checked_pairs": n, "checked_pairs_scalar": 0, "mismatches": mism, "bit_exact": mism == 0}
 
 
 def cut_roofline(ctx, dev, stream):
@@ -326,8 +344,10 @@ def main():
 
         cpu = None
         parity = None
-        if args.cpu_seconds > 0:
+        if args.cpu_seconds > 0 and world == 1:
             cpu, parity = cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j)
+        elif args.cpu_seconds > 0:
+            parity = parity_sample(batch, scoring, gpu_scores, gpu_i, gpu_j)
 
         # PCIe-inclusive rates (never `value`): the same batch from host memory,
         # scores back on the host, best of 3 calls per variant:
@@ -338,8 +358,8 @@ def main():
         #                  (here: the batch's windows laid end to end, so the
         #                  cells and scores are the same pairs')
         # each with the default chunking and with 4 chunks (copy/kernel overlap).
-        pcie = None
-        if not args.no_pcie:
+        pcie = cut = None
+        if not args.no_pcie and world == 1:
             pcie = pcie_rates(ctx, batch, scoring, cells, gpu_scores)
             cut = cut_roofline(ctx, dev, stream)
 
@@ -379,7 +399,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "pcie_inclusive": pcie,
-            "cut_windows_roofline": cut if not args.no_pcie else None,
+            "cut_windows_roofline": cut,
             "gathered_scores": gathered,
         }
         print(json.dumps(line), flush=True)
