@@ -111,6 +111,58 @@ def config_batch(k: int, n_pairs: int = 0, seed_offset: int = 0) -> PairBatch:
     raise ValueError(f"unknown config {k}")
 
 
+SHARD_BLOCK = 1024  # pairs per independently seeded block of a global batch
+
+
+def _config_shape(k: int):
+    """(read length spec, win_factor, read_stride, win_stride) of config k."""
+    if k in (2, 3, 4):
+        return 150, 2.0, 160, 304
+    if k == 5:
+        return (75, 250), 2.0, 256, 512
+    raise ValueError(f"no sharded form for config {k}")
+
+
+def config_block(k: int, blk: int, genome_arr: np.ndarray | None = None) -> PairBatch:
+    """Block ``blk`` (pairs [blk * SHARD_BLOCK, (blk + 1) * SHARD_BLOCK)) of
+    config k's global batch.  Its content depends only on (k, blk): the genome
+    comes from seed 1000 + k, the pairs from seed [1000 + k, blk]."""
+    seed = 1000 + k
+    g = config_genome(k) if genome_arr is None else genome_arr
+    rl, wf, rs, ws = _config_shape(k)
+    return make_pairs(SHARD_BLOCK, rl, wf, seed=[seed, blk], genome_arr=g, read_stride=rs, win_stride=ws)
+
+
+_GENOMES: dict = {}
+
+
+def config_genome(k: int, n_bases: int = 1 << 22) -> np.ndarray:
+    """The shared genome of config k's global batch (cached per process)."""
+    if k not in _GENOMES:
+        _GENOMES[k] = genome(n_bases, np.random.default_rng(1000 + k))
+    return _GENOMES[k]
+
+
+def config_shard(k: int, a: int, b: int) -> PairBatch:
+    """Pairs [a, b) of config k's GLOBAL seeded batch (bench.py's multi-GPU
+    form): pair i is the same whichever rank generates it and however many
+    ranks share the batch, so rank r scores ``shard_range(B, r, N)`` of one
+    batch and the gathered scores can be checked pair by pair."""
+    if b <= a:
+        rl, wf, rs, ws = _config_shape(k)
+        z = np.zeros((0,), np.uint16)
+        return PairBatch(np.zeros((0, rs), np.uint8), z, np.zeros((0, ws), np.uint8), z.copy(),
+                         np.zeros((0,), np.int64))
+    g = config_genome(k)
+    first, last = a // SHARD_BLOCK, (b - 1) // SHARD_BLOCK
+    parts = [config_block(k, blk, g) for blk in range(first, last + 1)]
+    lo = a - first * SHARD_BLOCK
+    hi = lo + (b - a)
+    cat = lambda f: np.ascontiguousarray(np.concatenate([f(p) for p in parts])[lo:hi])  # noqa: E731
+    return PairBatch(cat(lambda p: p.reads), cat(lambda p: p.read_len), cat(lambda p: p.wins),
+                     cat(lambda p: p.win_len), cat(lambda p: p.pos))
+
+
 BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 
 

@@ -43,3 +43,16 @@ def test_bench_json_line():
     assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] in ("port", "reference")
     assert cpu["sample"]
     assert d["parity"]["bit_exact"] is True and d["parity"]["mismatches"] == 0
+
+
+@pytest.mark.gpu
+def test_bench_more_gpus_than_visible_fails():
+    """On the 1-GPU box `bench.py --gpus 2` must exit non-zero with a message
+    (never a quiet n_gpus = 1 line)."""
+    import torch
+    n = torch.cuda.device_count()
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(max(n + 1, 2)), "--steps", "1", "--warmup", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "GPU(s) are visible" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -1,0 +1,102 @@
+"""bench.py's multi-rank path on the CPU (gloo, world size 2).
+
+The driver runs ``python -m torch.distributed.run --nproc-per-node N bench.py
+--gpus N`` (and a plain ``python bench.py --gpus N`` must start N ranks
+itself).  With ``--cpu-standin`` the ranks use gloo and a stand-in scorer, so
+these tests check the launcher, the sharding of ONE global batch, the
+max-over-ranks / sum-over-ranks bookkeeping and the ordered gather without a
+GPU.  Without a GPU, asking for 2 GPUs must fail loudly (exit status 3).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import standin_scores  # noqa: E402
+from mini_parallel_amd.synthetic import config_shard  # noqa: E402
+
+ARGS = ["--cpu-standin", "--steps", "2", "--warmup", "1", "--pairs", "3000", "--cpu-seconds", "0",
+        "--no-pcie", "--extra-configs", ""]
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _json_line(out):
+    lines = [l for l in out.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _check(d, world, per_gpu=3000):
+    assert d["n_gpus"] == world
+    assert d["config"]["global_pairs"] == per_gpu * world
+    assert d["gathered_scores"]["pairs"] == per_gpu * world
+    want = standin_scores(config_shard(2, 0, per_gpu * world))
+    got = np.array(d["standin_scores"], dtype=np.int32)
+    assert np.array_equal(got, want), "gather out of order or shards overlap"
+    assert d["config"]["cells_per_job_step"] == config_shard(2, 0, per_gpu * world).cells
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_self_launch_two_ranks():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + ARGS, cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check(_json_line(r.stdout), 2)
+
+
+def test_torchrun_two_ranks():
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2"]
+                       + ARGS, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check(_json_line(r.stdout), 2)
+
+
+def test_single_rank_standin():
+    r = subprocess.run([sys.executable, "bench.py"] + ARGS, cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check(_json_line(r.stdout), 1)
+
+
+def test_shards_of_one_global_batch():
+    """Pair i of the global batch is the same whichever range generates it."""
+    whole = config_shard(5, 0, 2500)
+    for a, b in ((0, 1), (1000, 1100), (1023, 1025), (2048, 2500)):
+        s = config_shard(5, a, b)
+        assert np.array_equal(s.reads, whole.reads[a:b]) and np.array_equal(s.wins, whole.wins[a:b])
+        assert np.array_equal(s.read_len, whole.read_len[a:b])
+    assert config_shard(2, 7, 7).n_pairs == 0
+
+
+def test_too_few_gpus_fails_loudly():
+    """--gpus larger than the visible GPU count: non-zero exit and a message,
+    never a quiet n_gpus = 1 line (here: no GPU at all; on a 1-GPU box the
+    GPU variant in test_bench_contract.py asks for 2)."""
+    import torch
+    n = torch.cuda.device_count()
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(max(n + 1, 2)), "--steps", "1", "--warmup", "0"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "GPU(s) are visible" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
