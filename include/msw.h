@@ -205,6 +205,22 @@ int msw_memcpy_h2d(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
 int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
 int msw_synchronize(msw_ctx* ctx);
 
+/* Counters of the host-batch calls (msw_align_batch*, msw_align_reads*) on a
+ * context, for run records (the reference's BenchmarkResult,
+ * tools/benchmark.rs:17-34, reports only wall-clock rates):
+ * kernel_ms = GPU time of the scoring launches (HIP events on the compute
+ * stream around each chunk's launch, added when the chunk is drained),
+ * alg_bytes = read + window bytes + 4 B score (+ 4 B coordinates) per pair,
+ * the kernel's algorithmic HBM traffic.  reset != 0 zeroes them after the copy. */
+typedef struct {
+    double kernel_ms;
+    uint64_t launches;
+    uint64_t pairs;
+    uint64_t cells;
+    uint64_t alg_bytes;
+} msw_stats_t;
+int msw_ctx_stats(msw_ctx* ctx, msw_stats_t* out, int reset);
+
 /* Thread-local message of the last failing call on this thread. */
 const char* msw_last_error(void);
 

@@ -37,6 +37,16 @@ void msw_fastq_close(msw_fastq* fq);
 int msw_fastq_next(msw_fastq* fq, uint8_t* seqs, uint16_t* lens, uint32_t stride,
                    uint64_t max_reads, uint64_t* n_read, int64_t* pos);
 
+/* Packed form, for callers that concatenate a chunk's sequences (the compat
+ * driver: chunk.concat() at aligner.rs:270, any read length): up to max_reads
+ * sequences appended back to back into buf[0, cap), lengths in lens[].  Stops
+ * early when the next sequence does not fit the space left; *need (optional)
+ * is then its length and the next call delivers it first (grow the buffer by
+ * at least that).  *n_bytes = bytes written; *n_read = 0 and *need = 0 at end
+ * of file. */
+int msw_fastq_next_packed(msw_fastq* fq, uint8_t* buf, uint64_t cap, uint32_t* lens, uint64_t max_reads,
+                          uint64_t* n_read, uint64_t* n_bytes, uint64_t* need);
+
 /* Counters so far: lines (valid lines, aligner.rs:136), reads, read errors. */
 void msw_fastq_stats(const msw_fastq* fq, uint64_t* lines, uint64_t* reads, uint64_t* errors);
 

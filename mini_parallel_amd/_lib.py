@@ -28,11 +28,11 @@ EXPORTED = (
     "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
     "msw_plan_create", "msw_align_batch_planned", "msw_plan_destroy",
     "msw_genome_create", "msw_genome_destroy", "msw_genome_length", "msw_align_reads",
-    "msw_align_reads_async", "msw_genome_cut_device",
+    "msw_align_reads_async", "msw_genome_cut_device", "msw_ctx_stats",
 )
 # include/msw_fastq.h
-FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_stats",
-                  "msw_fastq_count_bases")
+FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_next_packed",
+                  "msw_fastq_stats", "msw_fastq_count_bases")
 
 
 class MswError(RuntimeError):
@@ -71,6 +71,11 @@ class DeviceInfoT(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 256), ("mem_bytes", ctypes.c_uint64),
                 ("mem_free_bytes", ctypes.c_uint64), ("max_wg", ctypes.c_uint32),
                 ("cu_count", ctypes.c_uint32), ("arch", ctypes.c_char * 64)]
+
+
+class StatsT(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("launches", ctypes.c_uint64), ("pairs", ctypes.c_uint64),
+                ("cells", ctypes.c_uint64), ("alg_bytes", ctypes.c_uint64)]
 
 
 _lib = None
@@ -113,12 +118,15 @@ def _declare(L):
         "msw_memcpy_h2d": (I, [P, P, ctypes.c_size_t]),
         "msw_memcpy_d2h": (I, [P, P, ctypes.c_size_t]),
         "msw_synchronize": (I, [P]),
+        "msw_ctx_stats": (I, [P, ctypes.POINTER(StatsT), I]),
         "msw_last_error": (ctypes.c_char_p, []),
         "msw_version": (ctypes.c_char_p, []),
         "msw_fastq_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "msw_fastq_close": (None, [P]),
         "msw_fastq_next": (I, [P, P, P, ctypes.c_uint32, ctypes.c_uint64,
                                ctypes.POINTER(ctypes.c_uint64), P]),
+        "msw_fastq_next_packed": (I, [P, P, ctypes.c_uint64, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "msw_fastq_stats": (None, [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                    ctypes.POINTER(ctypes.c_uint64)]),
         "msw_fastq_count_bases": (I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),

@@ -25,8 +25,8 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from ._lib import (MSW_E_INVALID, BatchT, DeviceInfoT, MswError, OutT, ReadBatchT, ScoringT, check,
-                   lib)
+from ._lib import (MSW_E_INVALID, BatchT, DeviceInfoT, MswError, OutT, ReadBatchT, ScoringT, StatsT,
+                   check, lib)
 
 GPU_WORK_GROUP_SIZE = 1024          # gpu.rs:9
 GPU_MAX_WORK_GROUPS = 1_000_000     # gpu.rs:10
@@ -282,6 +282,14 @@ class Context:
     def synchronize(self) -> None:
         check(lib().msw_synchronize(self.handle))
 
+    def stats(self, reset: bool = False) -> dict:
+        """msw_ctx_stats: kernel time, launches, pairs, cells and algorithmic
+        bytes of this context's host-batch calls (since creation / last reset)."""
+        st = StatsT()
+        check(lib().msw_ctx_stats(self.handle, ctypes.byref(st), 1 if reset else 0))
+        return {"kernel_ms": st.kernel_ms, "launches": st.launches, "pairs": st.pairs, "cells": st.cells,
+                "alg_bytes": st.alg_bytes}
+
     # -- legacy kernel ------------------------------------------------------------------
     def compat(self, s1: bytes, s2: bytes, wg: int = 0, max_groups: int = 0) -> int:
         """smith_waterman_align semantics (see gpu_align)."""
@@ -294,9 +302,11 @@ class Context:
 
 
 class Pending:
-    """An asynchronous call in flight (msw_*_async ticket).  The input arrays
-    are held until ``wait()``; ``wait()`` returns (score, end_i, end_j).
-    Waiting on a ticket also completes every earlier one (msw_wait)."""
+    """An asynchronous call in flight (msw_*_async ticket).  The input and
+    output arrays are held until ``wait()``; ``wait()`` returns (score, end_i,
+    end_j).  Waiting on a ticket also completes every earlier one (msw_wait).
+    A Pending dropped without ``wait()`` waits in its finaliser: the runtime's
+    staging slots still point at its arrays until the ticket drains."""
 
     def __init__(self, ctx: "Context", ticket: int, outs, keep):
         self.ctx, self.ticket, self._outs, self._keep = ctx, ticket, outs, keep
@@ -306,6 +316,14 @@ class Pending:
             check(lib().msw_wait(self.ctx.handle, self.ticket))
             self._keep = None
         return self._outs
+
+    def __del__(self):
+        try:
+            if self._keep is not None and getattr(self.ctx, "_h", None) is not None:
+                lib().msw_wait(self.ctx._h, self.ticket)
+        except Exception:
+            pass
+        self._keep = None
 
 
 class Genome:

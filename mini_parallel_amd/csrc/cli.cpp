@@ -35,6 +35,7 @@
 #include <string>
 #include <thread>
 #include <fcntl.h>
+#include <sched.h>
 #include <unistd.h>
 #include <ctime>
 #include <vector>
@@ -77,6 +78,27 @@ void load_dotenv() {
             v = v.substr(1, v.size() - 2);
         setenv(k.c_str(), v.c_str(), 0);
     }
+}
+
+// CPUs this process may use: the affinity mask, capped by the cgroup v2 CPU
+// quota (cpu.max) when there is one.  The GPU boxes grant a 16-CPU quota on a
+// 256-CPU affinity mask, so hardware_concurrency() alone overstates it 16x.
+int usable_cpus() {
+    int n = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[64] = {0};
+        double period = 0;
+        if (fscanf(f, "%63s %lf", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const int quota = (int)(atof(q) / period);
+            if (quota >= 1) n = std::min(n, quota);
+        }
+        fclose(f);
+    }
+    return std::max(1, n);
 }
 
 // aligner.rs:9-15
@@ -418,7 +440,8 @@ class SlabPool {
 struct Chunk {
     size_t file_index = 0;
     SlabPool* pool = nullptr;
-    SlabPool::Slab* slab = nullptr;  // reads n x kReadStride, rlen, pos
+    SlabPool::Slab* slab = nullptr;  // sw: reads n x kReadStride, rlen, pos
+    std::vector<uint8_t> cat;        // compat: the chunk's sequences back to back (any read length)
     uint64_t n = 0;
     uint64_t first_read = 0;         // index of the chunk's first read in its file
     bool last = false;               // last chunk of its file
@@ -479,7 +502,37 @@ struct WgsReport {
     double wall_ms = 0;
     unsigned long long cells = 0;
     int readers = 0;
+    int host_threads = 0;
+    std::vector<msw_stats_t> gpu;  // per worker: kernel time and algorithmic bytes (msw_ctx_stats)
 };
+
+// GPU contexts of the --full-wgs workers: --num-gpus N of the visible devices,
+// or the ordinals listed in MSW_DEVICES (comma separated; an ordinal may
+// repeat: "0,0" runs two workers, each with its own context, on GPU 0 -- the
+// multi-worker path on a one-GPU box).
+std::vector<Device> worker_devices(const std::vector<Device>& devs, int n) {
+    std::vector<Device> pool;
+    const char* v = getenv("MSW_DEVICES");
+    if (v && *v) {
+        std::stringstream ss(v);
+        std::string tok;
+        while (std::getline(ss, tok, ',')) {
+            char* end = nullptr;
+            const long k = strtol(tok.c_str(), &end, 10);
+            if (tok.empty() || *end || k < 0 || k >= (long)devs.size())
+                die("error: MSW_DEVICES entry '" + tok + "' is not a visible GPU ordinal");
+            pool.push_back(devs[(size_t)k]);
+        }
+    } else {
+        pool = devs;
+    }
+    if (n < 1) die("error: --num-gpus must be >= 1");
+    if (n > (int)pool.size())
+        die("error: --num-gpus " + std::to_string(n) + " but only " + std::to_string(pool.size()) +
+            " GPU context(s) available (visible GPUs, or MSW_DEVICES)");
+    pool.resize((size_t)n);
+    return pool;
+}
 
 WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const std::vector<std::string>& files,
                        Checkpoint& ckpt) {
@@ -491,7 +544,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         genome = load_fasta(a.reference);
         printf("Loaded reference: %zu bases\n", genome.size());
     }
-    const int ngpu = std::max(1, std::min<int>(a.num_gpus, (int)devices.size()));
+    const int ngpu = (int)devices.size();  // already worker_devices(): one worker per entry
+    std::vector<msw_stats_t> gstats((size_t)ngpu);
     std::vector<std::unique_ptr<FileState>> st(files.size());
     std::vector<size_t> todo;
     for (size_t i = 0; i < files.size(); ++i) {
@@ -538,10 +592,11 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     // Readers: one thread per lane file in flight (a gzip stream inflates on
     // one core; zlib gives ~0.5-0.75 M reads/s per thread, far below what one
     // GPU scores, so the host side wants every file open at once).  Default
-    // min(files, MSW_HOST_THREADS) -- the host CPU share, default 16 -- or
-    // MSW_READERS.
+    // min(files, MSW_HOST_THREADS) -- the CPUs this process may use
+    // (usable_cpus()) -- or MSW_READERS.
     std::atomic<size_t> next_file{0};
-    const int host_threads = std::max(1, atoi(env_or("MSW_HOST_THREADS", "16").c_str()));
+    const int host_threads =
+        std::max(1, atoi(env_or("MSW_HOST_THREADS", std::to_string(usable_cpus())).c_str()));
     const int want_readers = std::max(1, atoi(env_or("MSW_READERS", std::to_string(host_threads).c_str()).c_str()));
     const int nreaders = std::max(1, std::min<int>((int)todo.size(), std::max(want_readers, 2 * ngpu)));
     // Fewer files than the CPU share: BGZF blocks of one file inflate on
@@ -582,10 +637,32 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     std::unique_ptr<Chunk> c(new Chunk());
                     c->file_index = fi;
                     c->first_read = reads_so_far;
-                    c->pool = &slabs;
-                    c->slab = slabs.get();
-                    if (msw_fastq_next(fq, c->slab->reads, c->slab->rlen, kReadStride, chunk, &c->n,
-                                       c->slab->pos) != MSW_OK) {
+                    bool ok = true;
+                    if (sw) {
+                        c->pool = &slabs;
+                        c->slab = slabs.get();
+                        ok = msw_fastq_next(fq, c->slab->reads, c->slab->rlen, kReadStride, chunk, &c->n,
+                                            c->slab->pos) == MSW_OK;
+                    } else {
+                        // compat: exactly `chunk` reads of any length, concatenated
+                        // (aligner.rs:270); the buffer grows when a read does not fit
+                        std::vector<uint8_t>& cat = c->cat;
+                        cat.resize((size_t)std::min<uint64_t>(chunk, 65536) * 160);
+                        std::vector<uint32_t> lens((size_t)std::min<uint64_t>(chunk, 65536));
+                        uint64_t used = 0;
+                        while (ok && c->n < chunk) {
+                            uint64_t got = 0, nb = 0, need = 0;
+                            const uint64_t want = std::min<uint64_t>(chunk - c->n, lens.size());
+                            ok = msw_fastq_next_packed(fq, cat.data() + used, cat.size() - used, lens.data(), want,
+                                                       &got, &nb, &need) == MSW_OK;
+                            used += nb;
+                            c->n += got;
+                            if (ok && need) cat.resize(std::max(2 * cat.size(), (size_t)(used + need)));
+                            else if (ok && got < want) break;  // end of file
+                        }
+                        cat.resize((size_t)used);
+                    }
+                    if (!ok) {
                         f.error = msw_last_error();
                         fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
                         f.failed = true;
@@ -668,7 +745,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 if (!c) break;
                 FileState& f = *st[c->file_index];
                 unsigned long long nb = 0;
-                for (uint64_t i = 0; i < c->n; ++i) nb += c->rlen()[i];
+                if (sw)
+                    for (uint64_t i = 0; i < c->n; ++i) nb += c->rlen()[i];
+                else
+                    nb = c->cat.size();
                 if (sw) {
                     // window = reference[pos : pos + W] (W = --window or 2 x read
                     // length, at most the kernel's 4096), clipped at the genome end
@@ -700,12 +780,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 } else {
                     // compat: chunk concat self-aligned (aligner.rs:269-276, :365-373)
                     long long chunk_score = 0;
-                    std::string cat;
-                    cat.reserve(nb);
-                    for (uint64_t i = 0; i < c->n; ++i) cat.append((const char*)c->reads() + i * kReadStride, c->rlen()[i]);
+                    const std::vector<uint8_t>& cat = c->cat;
                     if (cat.size() >= 1000) {
                         int32_t s = 0;
-                        if (msw_align_compat(ctx.h, (const uint8_t*)cat.data(), cat.size(), (const uint8_t*)cat.data(),
+                        if (msw_align_compat(ctx.h, cat.data(), cat.size(), cat.data(),
                                              cat.size(), std::min<uint32_t>(devices[g].max_wg, 1024), 1000000,
                                              &s) != MSW_OK) {
                             fprintf(stderr, "  GPU %d alignment error: %s\n", g, msw_last_error());
@@ -724,6 +802,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 pending.pop_front();
             }
             msw_genome_destroy(gen);
+            msw_ctx_stats(ctx.h, &gstats[(size_t)g], 0);
         });
     }
     for (auto& t : readers) t.join();
@@ -733,6 +812,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     rep.wall_ms = ms_since(t_all);
     rep.cells = cells.load();
     rep.readers = nreaders;
+    rep.host_threads = host_threads;
+    rep.gpu = gstats;
     for (size_t i = 0; i < files.size(); ++i)
         if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
     return rep;
@@ -742,8 +823,12 @@ std::string stable_run_id(const std::string& dir, const std::string& sample, con
     const char* v = getenv("WGS_RUN_ID");
     if (v && *v) return v;
     // FNV-1a over the inputs that define the run: same dataset + mode -> same id.
+    // The scoring scheme and window are part of it: a checkpoint written under
+    // other parameters is never resumed into this run.
     std::string key = dir + "|" + sample + "|" + a.score_mode + "|" + a.gap_model + "|" + a.reference + "|" +
-                      env_or("GPU_CHUNK_SIZE_READS", "");
+                      env_or("GPU_CHUNK_SIZE_READS", "") + "|" + std::to_string(a.match) + "|" +
+                      std::to_string(a.mismatch) + "|" + std::to_string(a.gap_open) + "|" +
+                      std::to_string(a.gap_extend) + "|" + std::to_string(a.window);
     uint64_t h = 1469598103934665603ull;
     for (unsigned char c : key) { h ^= c; h *= 1099511628211ull; }
     char buf[32];
@@ -787,7 +872,8 @@ int main(int argc, char** argv) {
         ck.path = a.checkpoint_dir + "/checkpoint_" + ck.run_id + ".json";
         ck.total_files = files.size();
         if (ck.load()) printf("Resuming run %s from %s\n", ck.run_id.c_str(), ck.path.c_str());
-        const WgsReport rep = run_full_wgs(a, devices, files, ck);
+        const std::vector<Device> workers = worker_devices(devices, a.num_gpus);
+        const WgsReport rep = run_full_wgs(a, workers, files, ck);
         long long total = 0;
         unsigned long long reads = 0, bases = 0;
         bool all_ok = true;
@@ -805,8 +891,9 @@ int main(int argc, char** argv) {
         if (rep.cells) printf(", %.1f GCUPS end-to-end", rep.cells / (rep.wall_ms * 1e6));
         printf("\n");
         // Run record: the reference's BenchmarkResult fields (tools/benchmark.rs:17-34;
-        // its fake gpu_utilization_avg / gpu_memory_used_mb are dropped) plus GCUPS.
-        const int ng = std::max(1, std::min<int>(a.num_gpus, (int)devices.size()));
+        // its fake gpu_utilization_avg / gpu_memory_used_mb are dropped) plus GCUPS
+        // (kernel and end to end), HBM GB/s and roofline fractions.
+        const int ng = (int)workers.size();
         const double secs = std::max(rep.wall_ms / 1000.0, 1e-9);
         char ts[64];
         {
@@ -822,7 +909,26 @@ int main(int argc, char** argv) {
             double v = 0;
             if (mi >> k >> v && k == "MemTotal:") ram_gb = v / (1024.0 * 1024.0);
         }
-        const double gcups = rep.cells ? rep.cells / (rep.wall_ms * 1e6) : 0.0;
+        const double gcups_e2e = rep.cells ? rep.cells / (rep.wall_ms * 1e6) : 0.0;
+        // Kernel rate: the job's cells over the busiest GPU's kernel time
+        // (HIP events around every chunk's scoring launch, msw_ctx_stats).
+        double kmax = 0, ksum = 0;
+        unsigned long long alg = 0;
+        for (const msw_stats_t& g : rep.gpu) {
+            kmax = std::max(kmax, g.kernel_ms);
+            ksum += g.kernel_ms;
+            alg += g.alg_bytes;
+        }
+        const bool sw_mode = a.score_mode == "sw";
+        const double gcups = kmax > 0 && sw_mode ? rep.cells / (kmax * 1e6) : 0.0;
+        const double hbm_gbps = kmax > 0 ? alg / (kmax * 1e6) : 0.0;
+        // Per-GPU ceilings: 8 TB/s HBM; VALU issue of the best-cell loops
+        // (128 cells per 30.28 / 46.99 cycles per packed row-step x 1024 SIMDs x
+        // 2.4 GHz; bench.py CYCLES_PER_ROW_STEP).
+        const double valu_ceiling = a.gap_model == "affine" ? 6694.5 : 10389.5;
+        const double frac_hbm = ng ? hbm_gbps / (8000.0 * ng) : 0.0;
+        const double frac_valu = ng && sw_mode ? gcups / (valu_ceiling * ng) : 0.0;
+        const double busy = ng && rep.wall_ms > 0 ? ksum / (ng * rep.wall_ms) : 0.0;
         std::ostringstream j;
         j << "{\"timestamp\": \"" << ts << "\", \"run_id\": \"" << ck.run_id << "\", \"mode\": \"full_wgs\""
           << ", \"score_mode\": \"" << a.score_mode << "\", \"files_processed\": " << rep.results.size()
@@ -835,7 +941,11 @@ int main(int argc, char** argv) {
           << "\", \"gpu_memory_gb\": " << (devices.empty() ? 0.0 : devices[0].memory_gb)
           << ", \"cpu_cores\": " << std::thread::hardware_concurrency() << ", \"total_ram_gb\": " << ram_gb << "}"
           << ", \"num_gpus\": " << ng << ", \"host_cores\": " << std::thread::hardware_concurrency()
-          << ", \"cells\": " << rep.cells << ", \"gcups\": " << gcups << ", \"gcups_end_to_end\": " << gcups
+          << ", \"host_cpus_usable\": " << usable_cpus() << ", \"host_threads\": " << rep.host_threads
+          << ", \"cells\": " << rep.cells << ", \"gcups\": " << gcups << ", \"gcups_end_to_end\": " << gcups_e2e
+          << ", \"kernel_ms\": " << kmax << ", \"gpu_busy_fraction\": " << busy
+          << ", \"alg_bytes\": " << alg << ", \"hbm_gbps\": " << hbm_gbps
+          << ", \"roofline_fraction_hbm\": " << frac_hbm << ", \"roofline_fraction_valu\": " << frac_valu
           << ", \"reads_per_second\": " << reads / secs << "}\n";
         write_json(a.json, j.str());
         return all_ok ? 0 : 1;
@@ -909,6 +1019,11 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> r(rs, 0), w(ws, 0);
         memcpy(r.data(), a.seq1.data(), a.seq1.size());
         memcpy(w.data(), a.seq2.data(), a.seq2.size());
+        if (a.seq1.size() > 0xFFFF || a.seq2.size() > 0xFFFF) {
+            fprintf(stderr, "GPU alignment error: sequence of %zu / %zu bases exceeds the kernel limits "
+                            "(read <= 256, window <= 4096)\n", a.seq1.size(), a.seq2.size());
+            return 1;
+        }
         uint16_t rl = (uint16_t)a.seq1.size(), wl = (uint16_t)a.seq2.size();
         int32_t score = 0;
         int16_t ei = -1, ej = -1;

@@ -43,6 +43,8 @@ struct msw_fastq {
     std::string last;         // final line of a file without a trailing newline
     uint64_t lines = 0, reads = 0, errors = 0;
     int64_t pending_pos = -1; // pos= tag of the current record's header
+    std::string held;         // msw_fastq_next_packed: a sequence that did not fit the caller's buffer
+    bool has_held = false;
     std::string path;
 };
 
@@ -356,6 +358,47 @@ int msw_fastq_next(msw_fastq* fq, uint8_t* seqs, uint16_t* lens, uint32_t stride
         ++n;
     }
     *n_read = n;
+    return MSW_OK;
+}
+
+int msw_fastq_next_packed(msw_fastq* fq, uint8_t* buf, uint64_t cap, uint32_t* lens, uint64_t max_reads,
+                          uint64_t* n_read, uint64_t* n_bytes, uint64_t* need) {
+    if (!fq || !n_read || !n_bytes || (max_reads && (!lens || (cap && !buf))))
+        return set_error(MSW_E_INVALID, "NULL argument");
+    *n_read = 0;
+    *n_bytes = 0;
+    if (need) *need = 0;
+    uint64_t n = 0, at = 0;
+    while (n < max_reads) {
+        const char* seq;
+        size_t len;
+        if (fq->has_held) {
+            seq = fq->held.data();
+            len = fq->held.size();
+        } else {
+            int64_t p;
+            const int rc = next_sequence(fq, &seq, &len, &p, false);
+            if (rc < 0) return rc;
+            if (rc == 0) break;
+            if (len > 0xFFFFFFFFull)
+                return set_error(MSW_E_RANGE, "sequence of %zu bases at line %llu", len,
+                                 (unsigned long long)fq->lines);
+        }
+        if (len > cap - at) {  // delivered by a later call (the caller grows its buffer by *need)
+            if (!fq->has_held) {
+                fq->held.assign(seq, len);
+                fq->has_held = true;
+            }
+            if (need) *need = len;
+            break;
+        }
+        if (len) memcpy(buf + at, seq, len);
+        at += len;
+        lens[n++] = (uint32_t)len;
+        fq->has_held = false;
+    }
+    *n_read = n;
+    *n_bytes = at;
     return MSW_OK;
 }
 

@@ -166,6 +166,7 @@ struct Slot {
     int32_t *d_score = nullptr, *h_score = nullptr;
     int16_t *d_ei = nullptr, *d_ej = nullptr, *h_ei = nullptr, *h_ej = nullptr;
     hipEvent_t uploaded = nullptr, computed = nullptr, done = nullptr;
+    hipEvent_t k_start = nullptr, k_end = nullptr;  // timing events around the chunk's scoring launch
     bool busy = false;
     uint64_t ticket = 0;  // msw_align_*_async call that owns the chunk in flight
     // Pending readback bookkeeping.
@@ -214,10 +215,12 @@ struct msw_ctx {
     Slot slots[kSlots];
     uint64_t next_ticket = 1, done_ticket = 0;
     uint64_t slot_seq = 0;  // chunks submitted (slot = slot_seq % kSlots)
+    msw_stats_t stats{};    // msw_ctx_stats: host-batch calls since creation / the last reset
     // compat buffers
     uint8_t *c_s1 = nullptr, *c_s2 = nullptr;
     int32_t* c_res = nullptr;
     size_t c_cap = 0;
+    hipEvent_t c_k0 = nullptr, c_k1 = nullptr;  // timing of the compat launch (msw_ctx_stats)
 };
 
 struct msw_genome {
@@ -261,6 +264,8 @@ int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
         HIP_TRY(hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&s.computed, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreate(&s.k_start));
+        HIP_TRY(hipEventCreate(&s.k_end));
     }
     if (pairs > s.cap_pairs) {
         if ((rc = grow_dev(&s.d_meta, pairs * kMetaBytesPerPair)) ||
@@ -524,11 +529,15 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
     return MSW_OK;
 }
 
-// Copy finished results of a slot into the caller's arrays.
-int drain_slot(Slot& s) {
+// Copy finished results of a slot into the caller's arrays; the chunk's
+// kernel time goes into the context's counters.
+int drain_slot(msw_ctx* ctx, Slot& s) {
     if (!s.busy) return MSW_OK;
     s.busy = false;
     HIP_TRY(hipEventSynchronize(s.done));
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, s.k_start, s.k_end) == hipSuccess) ctx->stats.kernel_ms += ms;
+    else (void)hipGetLastError();
     memcpy(s.out.score + s.first, s.h_score, s.count * sizeof(int32_t));
     if (s.out.end_i) memcpy(s.out.end_i + s.first, s.h_ei, s.count * sizeof(int16_t));
     if (s.out.end_j) memcpy(s.out.end_j + s.first, s.h_ej, s.count * sizeof(int16_t));
@@ -608,9 +617,8 @@ struct HostTrace {
     }
 };
 
-int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out_t* out, uint64_t chunk_pairs,
-              bool sync) {
-    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out_t* out,
+                   uint64_t chunk_pairs, bool sync) {
     Scheme sch;
     int rc;
     if ((rc = make_scheme(sc, &sch))) return rc;
@@ -660,7 +668,7 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
         // Slots alternate across calls too, so consecutive async calls overlap.
         Slot& s = ctx->slots[ctx->slot_seq++ % msw_ctx::kSlots];
         if (tr.on) tr.submit += tr.lap();
-        if ((rc = drain_slot(s))) return rc;  // the slot's previous chunk must be out before reuse
+        if ((rc = drain_slot(ctx, s))) return rc;  // the slot's previous chunk must be out before reuse
         if (tr.on) tr.wait += tr.lap();
         if ((rc = ensure_slot(s, cnt, (size_t)cnt * rs, (size_t)cnt * ws))) return rc;
         set_views(s, cnt);
@@ -725,7 +733,20 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
             buckets.resize(1);
             buckets[0].begin = 0;
         }
+        HIP_TRY(hipEventRecord(s.k_start, ctx->compute));
         if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws))) return rc;
+        HIP_TRY(hipEventRecord(s.k_end, ctx->compute));
+        {
+            uint64_t cells = 0, bytes = 0;
+            for (uint64_t i = 0; i < cnt; ++i) {
+                cells += (uint64_t)s.h_rlen[i] * s.h_wlen[i];
+                bytes += (uint64_t)s.h_rlen[i] + s.h_wlen[i];
+            }
+            ctx->stats.launches += 1;
+            ctx->stats.pairs += cnt;
+            ctx->stats.cells += cells;
+            ctx->stats.alg_bytes += bytes + cnt * (sch.coords ? 8u : 4u);
+        }
         hipStream_t down = ctx->compute;
         if (multi_chunk) {
             HIP_TRY(hipEventRecord(s.computed, ctx->compute));
@@ -745,7 +766,7 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     if (sync) {
         if (tr.on) tr.submit += tr.lap();
         for (Slot& sl : ctx->slots)
-            if ((rc = drain_slot(sl))) return rc;
+            if ((rc = drain_slot(ctx, sl))) return rc;
         if (tr.on) tr.wait += tr.lap();
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
@@ -759,6 +780,32 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     return MSW_OK;
 }
 
+
+// A call that fails after submitting some of its chunks must not leave them
+// behind: they point at the caller's output arrays, and a later msw_wait or
+// slot reuse would drain them there (the caller may have freed them by then).
+// The streams are synchronised, the call's chunks dropped, and its ticket
+// number consumed so no later call shares it.
+int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out_t* out, uint64_t chunk_pairs,
+              bool sync) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    const uint64_t ticket = ctx->next_ticket;
+    const int rc = run_batch_impl(ctx, sc, b, out, chunk_pairs, sync);
+    if (rc == MSW_OK) return rc;
+    bool dropped = false;
+    for (Slot& s : ctx->slots) dropped = dropped || (s.busy && s.ticket == ticket);
+    if (dropped) {
+        const std::string msg = g_last_error;
+        (void)hipStreamSynchronize(ctx->copy);
+        (void)hipStreamSynchronize(ctx->compute);
+        (void)hipStreamSynchronize(ctx->d2h);
+        for (Slot& s : ctx->slots)
+            if (s.busy && s.ticket == ticket) s.busy = false;
+        ctx->next_ticket++;
+        g_last_error = msg;
+    }
+    return rc;
+}
 
 HostBatch pairs_batch(const msw_batch_t& b) {
     HostBatch h;
@@ -863,8 +910,12 @@ void msw_ctx_destroy(msw_ctx* ctx) {
         if (s.uploaded) (void)hipEventDestroy(s.uploaded);
         if (s.computed) (void)hipEventDestroy(s.computed);
         if (s.done) (void)hipEventDestroy(s.done);
+        if (s.k_start) (void)hipEventDestroy(s.k_start);
+        if (s.k_end) (void)hipEventDestroy(s.k_end);
         free_slot(s);
     }
+    if (ctx->c_k0) (void)hipEventDestroy(ctx->c_k0);
+    if (ctx->c_k1) (void)hipEventDestroy(ctx->c_k1);
     (void)hipFree(ctx->c_s1);
     (void)hipFree(ctx->c_s2);
     (void)hipFree(ctx->c_res);
@@ -898,7 +949,7 @@ int msw_wait(msw_ctx* ctx, uint64_t ticket) {
     // Drain the chunks of this ticket and of every earlier one (tickets are
     // enqueued in order on the same streams); later calls stay in flight.
     for (Slot& s : ctx->slots)
-        if (s.busy && s.ticket <= ticket && (rc = drain_slot(s))) return rc;
+        if (s.busy && s.ticket <= ticket && (rc = drain_slot(ctx, s))) return rc;
     ctx->done_ticket = std::max(ctx->done_ticket, ticket);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
@@ -1109,9 +1160,19 @@ int msw_align_compat(msw_ctx* ctx, const uint8_t* s1, size_t n1, const uint8_t* 
     HIP_TRY(hipMemcpyAsync(ctx->c_s1, s1, L, hipMemcpyHostToDevice, ctx->compute));
     HIP_TRY(hipMemcpyAsync(ctx->c_s2, s2, L, hipMemcpyHostToDevice, ctx->compute));
     HIP_TRY(hipMemsetAsync(ctx->c_res, 0, sizeof(int32_t), ctx->compute));
+    if (!ctx->c_k0) {
+        HIP_TRY(hipEventCreate(&ctx->c_k0));
+        HIP_TRY(hipEventCreate(&ctx->c_k1));
+    }
+    HIP_TRY(hipEventRecord(ctx->c_k0, ctx->compute));
     HIP_TRY(msw::launch_compat(ctx->c_s1, ctx->c_s2, ctx->c_res, L, W, G, ctx->compute));
+    HIP_TRY(hipEventRecord(ctx->c_k1, ctx->compute));
     HIP_TRY(hipMemcpyAsync(score, ctx->c_res, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->compute));
     HIP_TRY(hipStreamSynchronize(ctx->compute));
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, ctx->c_k0, ctx->c_k1) == hipSuccess) ctx->stats.kernel_ms += ms;
+    ctx->stats.launches += 1;
+    ctx->stats.alg_bytes += 2ull * L + 4;
     return MSW_OK;
 }
 
@@ -1225,6 +1286,13 @@ int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes) {
     int rc = set_device(ctx);
     if (rc) return rc;
     HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return MSW_OK;
+}
+
+int msw_ctx_stats(msw_ctx* ctx, msw_stats_t* out, int reset) {
+    if (!ctx || !out) return fail(MSW_E_INVALID, "ctx/out is NULL");
+    *out = ctx->stats;
+    if (reset) ctx->stats = msw_stats_t{};
     return MSW_OK;
 }
 

@@ -53,6 +53,35 @@ class FastqReader:
             return seqs[:k], lens[:k], pos[:k]
         return seqs[:k], lens[:k]
 
+    def next_packed(self, max_reads: int, cap: int):
+        """msw_fastq_next_packed: up to max_reads sequences back to back in a
+        buffer of cap bytes -> (buf u8[n_bytes], lens u32[n], need): ``need``
+        is the length of the next sequence when it did not fit (0 at end of
+        file or when max_reads were delivered)."""
+        buf = np.zeros(max(cap, 1), np.uint8)
+        lens = np.zeros(max(max_reads, 1), np.uint32)
+        n, nb, need = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(lib().msw_fastq_next_packed(self._h, buf.ctypes.data, cap, lens.ctypes.data, max_reads,
+                                          ctypes.byref(n), ctypes.byref(nb), ctypes.byref(need)))
+        return buf[:nb.value], lens[:n.value], int(need.value)
+
+    def next_concat(self, n_reads: int):
+        """Exactly n_reads sequences (fewer at end of file) of any length,
+        concatenated -- the chunk.concat() of aligner.rs:270 -- and their
+        lengths; the buffer grows when a sequence does not fit."""
+        parts, lens, got, cap = [], [], 0, max(1024, min(n_reads, 65536) * 160)
+        while got < n_reads:
+            buf, ln, need = self.next_packed(n_reads - got, cap)
+            parts.append(buf)
+            lens.append(ln)
+            got += len(ln)
+            if need:
+                cap = max(2 * cap, need)
+            elif got < n_reads:
+                break
+        cat = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        return cat, (np.concatenate(lens) if lens else np.zeros(0, np.uint32))
+
     def stats(self) -> dict:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         lib().msw_fastq_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
@@ -60,18 +89,22 @@ class FastqReader:
 
 
 def process_fastq_file_in_chunks(filepath: str, chunk_size_reads: int,
-                                 processor: Callable[[list], Optional[object]], stride: int = 4096) -> None:
-    """aligner.rs:107-178: call ``processor`` with lists of sequence strings,
-    full chunks of chunk_size_reads then one final partial chunk.  (For the
-    GPU path use FastqReader.next_chunk, which fills SoA slabs directly.)"""
+                                 processor: Callable[[list], Optional[object]]) -> None:
+    """aligner.rs:107-178: call ``processor`` with lists of sequence strings
+    (any length), full chunks of chunk_size_reads then one final partial
+    chunk.  (For the GPU path use FastqReader.next_chunk, which fills SoA
+    slabs directly, or next_concat for the compat driver's concatenation.)"""
     if chunk_size_reads <= 0:
         raise MswError(-1, "chunk_size_reads must be positive")
     with FastqReader(filepath) as fq:
         while True:
-            seqs, lens = fq.next_chunk(chunk_size_reads, stride)
+            cat, lens = fq.next_concat(chunk_size_reads)
             if len(lens) == 0:
                 break
-            processor([bytes(seqs[i, :lens[i]]).decode() for i in range(len(lens))])
+            ends = np.cumsum(lens.astype(np.int64))
+            starts = ends - lens
+            raw = cat.tobytes()
+            processor([raw[a:b].decode() for a, b in zip(starts, ends)])
 
 
 def count_bases_in_fastq(filepath: str) -> int:

@@ -161,3 +161,96 @@ def test_full_wgs_compat_and_test_wgs(tmp_path):
     assert r.returncode == 0
     got = [int(x) for x in re.findall(r"Successfully counted (\d+) bases", r.stdout)]
     assert got == [int(b.read_len.astype(int).sum()) for b in ds["batches"][:2]]
+
+
+REC_T = np.dtype([("score", "<i4"), ("end_i", "<i2"), ("end_j", "<i2")])
+
+
+@pytest.mark.gpu
+def test_full_wgs_config4_shape_two_workers(tmp_path, oracle):
+    """BASELINE config 4's shape (8 lanes x R1/R2 lane files of 150 bp reads,
+    300 bp windows), reduced to 2,000 reads per file, through the multi-worker
+    path: MSW_DEVICES=0,0 --num-gpus 2 builds two contexts on the one GPU, so
+    the shared chunk queue, the exactly-once file completion and per-chunk
+    pwrite from several workers all run.  Per-read records and per-file i64
+    sums equal the oracle's; the run record carries kernel and end-to-end
+    GCUPS, HBM GB/s and both roofline fractions; resume skips every file."""
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=8, reads_per_lane=2, reads_per_file=2000, bgzf=True,
+                           workers=4)
+    env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "8",
+           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "600", "WGS_RUN_ID": "c4", "MSW_DEVICES": "0,0"}
+    (tmp_path / "scores").mkdir()
+    args = ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
+            "--num-gpus", "2", "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json"),
+            "--scores-out", str(tmp_path / "scores")]
+    r = run(args, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    per_file = []
+    for f, b in zip(ds["files"], ds["batches"]):
+        s, i, j = oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=16)
+        per_file.append(int(s.astype(np.int64).sum()))
+        got = np.fromfile(tmp_path / "scores" / (os.path.basename(f) + ".scores"), dtype=REC_T)
+        assert np.array_equal(got["score"], s) and np.array_equal(got["end_i"], i) and np.array_equal(got["end_j"], j)
+    rec = json.load(open(tmp_path / "rec.json"))
+    assert rec["total_score"] == sum(per_file) and rec["total_reads"] == 16 * 2000
+    assert rec["num_gpus"] == 2 and rec["files_processed"] == 16
+    for k in ("gcups", "gcups_end_to_end", "hbm_gbps", "roofline_fraction_hbm", "roofline_fraction_valu",
+              "kernel_ms", "gpu_busy_fraction", "host_cpus_usable", "host_threads"):
+        assert k in rec, k
+    assert rec["gcups"] >= rec["gcups_end_to_end"] > 0
+    assert 0 < rec["roofline_fraction_hbm"] < 1 and 0 < rec["roofline_fraction_valu"] < 1
+    assert rec["hbm_gbps"] > 0 and rec["cells"] == sum(int((b.read_len.astype(np.int64) * 300).sum())
+                                                       for b in ds["batches"])
+    ck = json.load(open(tmp_path / "checkpoint_c4.json"))
+    assert [f["score"] for f in sorted(ck["files"], key=lambda f: f["file_index"])] == per_file
+    r2 = run(args, env=env, cwd=tmp_path)
+    assert r2.returncode == 0 and r2.stdout.count("Skipping completed file") == 16
+    assert json.load(open(tmp_path / "rec.json"))["total_score"] == sum(per_file)
+
+
+@pytest.mark.gpu
+def test_num_gpus_beyond_visible_fails(tmp_path):
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    import torch
+    write_wgs_dataset(str(tmp_path / "wgs"), lanes=1, reads_per_lane=1, reads_per_file=10)
+    env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "1",
+           "WGS_READS_PER_LANE": "1", "GPU_CHUNK_SIZE_READS": "10"}
+    r = run(["--full-wgs", "--gpu", "--num-gpus", str(torch.cuda.device_count() + 1)], env=env, cwd=tmp_path)
+    assert r.returncode == 1 and "GPU context(s) available" in r.stderr
+
+
+@pytest.mark.gpu
+def test_full_wgs_compat_long_reads(tmp_path):
+    """Compat mode concatenates reads of any length (aligner.rs:269-276):
+    MiSeq-like 2 x 300 bp reads -- and one 5 kb read -- no longer fail the
+    file (the sw slabs' 256 bp stride does not apply)."""
+    rng = np.random.default_rng(8)
+    alpha = np.frombuffer(b"ACGT", np.uint8)
+    wgs = tmp_path / "wgs"
+    wgs.mkdir()
+    lens = [300] * 23 + [5000] + [300] * 6
+    seqs = [bytes(rng.choice(alpha, k)).decode() for k in lens]
+    import gzip
+    with gzip.open(wgs / "SYN_L001_R1_001.fastq.gz", "wt") as f:
+        for i, s in enumerate(seqs):
+            f.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
+    env = {"WGS_DATA_DIR": str(wgs), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "1", "WGS_READS_PER_LANE": "1",
+           "GPU_CHUNK_SIZE_READS": "3", "WGS_RUN_ID": "long"}
+    r = run(["--full-wgs", "--gpu", "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "c.json")],
+            env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rec = json.load(open(tmp_path / "c.json"))
+    # every 3-read chunk has >= 1000 bases... except none: 3 x 300 = 900 < 1000, so only the chunk with the 5 kb read
+    want = sum(2 for k in range(0, len(lens), 3) if sum(lens[k:k + 3]) >= 1000)
+    assert rec["total_score"] == want and rec["total_reads"] == len(seqs)
+    assert rec["total_bases"] == sum(lens)
+
+
+@pytest.mark.gpu
+def test_pair_sw_oversize_is_range_error(tmp_path):
+    """A 70,000-base sequence must not wrap through the u16 length."""
+    r = run(["-1", "A" * 70000, "-2", "ACGT", "--gpu", "--score-mode", "sw"], cwd=tmp_path)
+    assert r.returncode == 1 and "exceeds the kernel limits" in r.stderr
+    r = run(["-1", "A" * 300, "-2", "ACGT", "--gpu", "--score-mode", "sw"], cwd=tmp_path)
+    assert r.returncode == 1 and "read length 300" in r.stderr

@@ -166,3 +166,37 @@ def test_bgzf_corrupt_block_is_an_error(tmp_path):
     open(p, "wb").write(bytes(blob))
     with pytest.raises(MswError):
         process_fastq_file_in_chunks(p, 100000, lambda c: None)
+
+
+@pytest.mark.parametrize("cap", [1, 64, 700, 1 << 20])
+def test_packed_reader_any_length(tmp_path, cap):
+    """msw_fastq_next_packed: sequences of any length (here up to 5000 bases,
+    longer than any slab stride) back to back; a sequence that does not fit
+    is held for the next call and reported through `need`."""
+    rng = np.random.default_rng(11)
+    seqs = [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), int(k)))
+            for k in rng.integers(0, 5000, 60)]
+    data = b"".join(b"@r%d\n%s\n+\n%s\n" % (i, s, b"I" * len(s)) for i, s in enumerate(seqs))
+    p = str(tmp_path / "long.fastq.gz")
+    write(p, data, True)
+    got = []
+    with FastqReader(p) as fq:
+        c = cap
+        while True:
+            buf, lens, need = fq.next_packed(7, c)
+            assert int(lens.sum()) == len(buf) <= c
+            ends = np.cumsum(lens.astype(np.int64))
+            got += [buf[e - l:e].tobytes() for e, l in zip(ends, lens)]
+            if need:
+                assert need == len(seqs[len(got)]) and need > c - len(buf)
+                c = max(c, need)
+            elif len(lens) == 0:
+                break
+    assert got == seqs
+    # the compat driver's chunks: exactly N reads concatenated, any length
+    with FastqReader(p) as fq:
+        cat, lens = fq.next_concat(25)
+    assert cat.tobytes() == b"".join(seqs[:25]) and list(lens) == [len(s) for s in seqs[:25]]
+    chunks = []
+    process_fastq_file_in_chunks(p, 25, chunks.append)
+    assert chunks == reference_chunks(data, 25)

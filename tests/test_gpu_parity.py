@@ -212,6 +212,35 @@ def test_async_and_chunking_agree(gpu_ctx, oracle):
             assert_same(gpu_run(gpu_ctx, b, sc, chunk), want, True)
 
 
+def test_dropped_pending_then_more_calls(gpu_ctx, oracle):
+    """an async call dropped without wait() must not leave chunks
+    that later drain into its freed output arrays (Pending.__del__ waits)."""
+    import gc
+    b = config_batch(2, n_pairs=3000, seed_offset=41)
+    sc = Scoring(want_coords=True)
+    want = oracle_run(oracle, b, sc)
+    for _ in range(3):
+        p = gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc, chunk_pairs=700, asynchronous=True)
+        del p
+        gc.collect()
+        junk = [np.full(3000, 7, np.int32) for _ in range(8)]  # reuse the freed memory
+        assert_same(gpu_run(gpu_ctx, b, sc, 1000), want, True)
+        assert all((j == 7).all() for j in junk)
+
+
+def test_ctx_stats_count_kernel_time(gpu_ctx):
+    """msw_ctx_stats: kernel time and algorithmic bytes of host-batch calls."""
+    b = config_batch(2, n_pairs=4000, seed_offset=42)
+    gpu_ctx.stats(reset=True)
+    gpu_run(gpu_ctx, b, Scoring(), 1000)
+    st = gpu_ctx.stats(reset=True)
+    assert st["launches"] == 4 and st["pairs"] == 4000
+    assert st["cells"] == int((b.read_len.astype(np.int64) * b.win_len).sum())
+    assert st["alg_bytes"] == int(b.read_len.astype(np.int64).sum() + b.win_len.astype(np.int64).sum()) + 4 * 4000
+    assert 0 < st["kernel_ms"] < 1000
+    assert gpu_ctx.stats()["launches"] == 0
+
+
 def test_empty_batch(gpu_ctx):
     R = np.zeros((0, 16), np.uint8)
     s, i, j = gpu_ctx.align_batch(R, np.zeros(0, np.uint16), R, np.zeros(0, np.uint16), Scoring(want_coords=True))
