@@ -58,6 +58,11 @@ struct SwParams {
     uint32_t f16_hi;          // high byte of f16(+match) | high byte of f16(mismatch) << 8
     uint32_t f16_ngap2;       // f16(-gap) (linear) / f16(-gap_extend) (affine), both halves
     uint32_t f16_noe2;        // affine: f16(-(gap_open + gap_extend)), both halves
+    // Results by slot (needs order): score[out_slot_base + slot] instead of
+    // score[pair], so each wave's stores are contiguous; the caller restores
+    // pair order (msw_runtime.cpp: the host drain, or launch_gather_results).
+    uint32_t out_by_slot;
+    uint32_t out_slot_base;
 };
 
 // f16 bits of the cell value v * 2^-11 (|v| < 2048: exact, normal or zero).
@@ -125,6 +130,13 @@ hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, 
 constexpr uint32_t kGenomePad = 64;
 hipError_t launch_cut_windows(const uint8_t* genome, uint64_t glen, const int64_t* pos, const uint16_t* want,
                               uint8_t* out, uint16_t* out_len, uint32_t ws, uint64_t n, hipStream_t stream);
+
+// dst[i] = src[inv[i]] for score (and end_i / end_j when non-null): pair
+// order restored from slot-ordered results (one thread per pair, coalesced
+// stores; the slot-ordered source is small enough to stay in L2).
+hipError_t launch_gather_results(const uint32_t* inv, const int32_t* src_score, const int16_t* src_i,
+                                 const int16_t* src_j, int32_t* score, int16_t* end_i, int16_t* end_j, uint64_t n,
+                                 hipStream_t stream);
 
 // smith_waterman_align restated: result must be zeroed before the launch.
 hipError_t launch_compat(const uint8_t* s1, const uint8_t* s2, int32_t* result, uint64_t L,

@@ -1,0 +1,23 @@
+// msw_launch.h -- per-translation-unit launchers of the SW kernel instance
+// set (internal; msw_kernels.hip dispatches to them).  Each msw_launch_*.hip
+// instantiates one disjoint slice of sw_kernel / sw_mixed_kernel /
+// sw_multi_kernel, so the slices compile in parallel.
+#pragma once
+#include "msw_kernels.h"
+
+namespace msw {
+
+// pairs layout, KR = 1..16 (msw_launch_pairs_lin.hip / msw_launch_pairs_aff.hip)
+hipError_t launch_pairs_lin(const SwParams& p, bool coords, int kr, hipStream_t stream);
+hipError_t launch_pairs_aff(const SwParams& p, bool coords, int kr, hipStream_t stream);
+// split layout, KR = 1..8 (msw_launch_split.hip)
+hipError_t launch_split(const SwParams& p, bool affine, bool coords, int kr, hipStream_t stream);
+// mixed grid, even KRP = 2..16 (msw_launch_mixed.hip)
+hipError_t launch_mixed(const SwParams& p, bool affine, bool coords, int krp, uint32_t blocks, hipStream_t stream);
+// length-bucketed grid (msw_launch_multi_lin.hip / msw_launch_multi_aff.hip)
+hipError_t launch_multi_lin(const SwParams& p, const MultiTable& t, bool coords, uint32_t grid, size_t shm,
+                            hipStream_t stream);
+hipError_t launch_multi_aff(const SwParams& p, const MultiTable& t, bool coords, uint32_t grid, size_t shm,
+                            hipStream_t stream);
+
+}  // namespace msw

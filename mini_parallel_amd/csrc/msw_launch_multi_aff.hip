@@ -1,0 +1,14 @@
+// msw_launch_multi_aff.hip -- length-bucketed SW grid, affine gap.
+#include "msw_device.h"
+#include "msw_launch.h"
+
+namespace msw {
+
+hipError_t launch_multi_aff(const SwParams& p, const MultiTable& t, bool coords, uint32_t grid, size_t shm,
+                            hipStream_t stream) {
+    if (coords) hipLaunchKernelGGL((sw_multi_kernel<true, true>), dim3(grid), dim3(64), shm, stream, p, t);
+    else hipLaunchKernelGGL((sw_multi_kernel<true, false>), dim3(grid), dim3(64), shm, stream, p, t);
+    return hipGetLastError();
+}
+
+}  // namespace msw

@@ -1,0 +1,14 @@
+// msw_launch_multi_lin.hip -- length-bucketed SW grid, linear gap.
+#include "msw_device.h"
+#include "msw_launch.h"
+
+namespace msw {
+
+hipError_t launch_multi_lin(const SwParams& p, const MultiTable& t, bool coords, uint32_t grid, size_t shm,
+                            hipStream_t stream) {
+    if (coords) hipLaunchKernelGGL((sw_multi_kernel<false, true>), dim3(grid), dim3(64), shm, stream, p, t);
+    else hipLaunchKernelGGL((sw_multi_kernel<false, false>), dim3(grid), dim3(64), shm, stream, p, t);
+    return hipGetLastError();
+}
+
+}  // namespace msw

@@ -168,6 +168,7 @@ struct Slot {
     hipEvent_t uploaded = nullptr, computed = nullptr, done = nullptr;
     hipEvent_t k_start = nullptr, k_end = nullptr;  // timing events around the chunk's scoring launch
     bool busy = false;
+    bool by_slot = false;  // results in slot order: the drain scatters them through h_order
     uint64_t ticket = 0;  // msw_align_*_async call that owns the chunk in flight
     // Pending readback bookkeeping.
     uint64_t first = 0, count = 0;
@@ -498,6 +499,8 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.win_vec = msw::vec_ok(p.wins, p.win_stride);
         p.group_lanes = 16;
         p.groups = 4;
+        p.out_by_slot = 1;
+        p.out_slot_base = 0;
         msw::MultiTable t;
         fill_multi(buckets, sch, t);
         HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
@@ -510,6 +513,8 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.read_len = s.d_rlen;
         p.win_len = s.d_wlen;
         p.order = use_order ? s.d_order + b.begin : nullptr;
+        p.out_by_slot = use_order ? 1u : 0u;
+        p.out_slot_base = b.begin;
         p.score = s.d_score;
         p.end_i = sch.coords ? s.d_ei : nullptr;
         p.end_j = sch.coords ? s.d_ej : nullptr;
@@ -538,6 +543,18 @@ int drain_slot(msw_ctx* ctx, Slot& s) {
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, s.k_start, s.k_end) == hipSuccess) ctx->stats.kernel_ms += ms;
     else (void)hipGetLastError();
+    if (s.by_slot) {  // length-bucketed chunk: slot k holds pair h_order[k]
+        int32_t* sc = s.out.score + s.first;
+        for (uint64_t k = 0; k < s.count; ++k) sc[s.h_order[k]] = s.h_score[k];
+        if (s.out.end_i) {
+            int16_t *ei = s.out.end_i + s.first, *ej = s.out.end_j + s.first;
+            for (uint64_t k = 0; k < s.count; ++k) {
+                ei[s.h_order[k]] = s.h_ei[k];
+                ej[s.h_order[k]] = s.h_ej[k];
+            }
+        }
+        return MSW_OK;
+    }
     memcpy(s.out.score + s.first, s.h_score, s.count * sizeof(int32_t));
     if (s.out.end_i) memcpy(s.out.end_i + s.first, s.h_ei, s.count * sizeof(int16_t));
     if (s.out.end_j) memcpy(s.out.end_j + s.first, s.h_ej, s.count * sizeof(int16_t));
@@ -757,6 +774,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
                                down));
         HIP_TRY(hipEventRecord(s.done, down));
         s.busy = true;
+        s.by_slot = !uniform;
         s.ticket = ctx->next_ticket;  // the ticket an async call returns
         s.first = first;
         s.count = cnt;
@@ -1030,6 +1048,13 @@ struct msw_plan {
     uint64_t n = 0;
     uint32_t max_m = 0, max_n = 0;
     uint32_t* d_order = nullptr;
+    // Non-identity order: the kernel writes results in slot order into d_tmp
+    // (score i32 | end_i i16 | end_j i16, n each) and a gather pass puts them
+    // in pair order through d_inv (pair -> slot): coalesced stores instead of
+    // one scattered 4-byte store per pair.
+    bool identity = true;
+    uint32_t* d_inv = nullptr;
+    uint8_t* d_tmp = nullptr;
     bool multi = false;
     msw::MultiTable table{};
     LaunchPlan single{};
@@ -1071,6 +1096,15 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
         hipError_t e = rc ? hipSuccess : hipMemcpy(pl->d_order, order.data(), n_pairs * sizeof(uint32_t),
                                                    hipMemcpyHostToDevice);
         if (!rc && e != hipSuccess) rc = fail(MSW_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+        for (uint64_t k = 0; k < n_pairs && pl->identity; ++k) pl->identity = order[k] == (uint32_t)k;
+        if (!rc && !pl->identity) {
+            std::vector<uint32_t> inv(n_pairs);
+            for (uint64_t k = 0; k < n_pairs; ++k) inv[order[k]] = (uint32_t)k;
+            if (!(rc = grow_dev(&pl->d_inv, n_pairs)) && !(rc = grow_dev(&pl->d_tmp, n_pairs * kResBytesPerPair))) {
+                e = hipMemcpy(pl->d_inv, inv.data(), n_pairs * sizeof(uint32_t), hipMemcpyHostToDevice);
+                if (e != hipSuccess) rc = fail(MSW_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+            }
+        }
         if (rc) {
             msw_plan_destroy(pl);
             return rc;
@@ -1107,27 +1141,42 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
     p.win_stride = b->win_stride;
     p.win_vec = msw::vec_ok(p.wins, p.win_stride);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    const uint64_t n = plan->n;
+    int32_t* t_score = reinterpret_cast<int32_t*>(plan->d_tmp);
+    int16_t* t_i = reinterpret_cast<int16_t*>(plan->d_tmp + 4 * n);
+    int16_t* t_j = reinterpret_cast<int16_t*>(plan->d_tmp + 6 * n);
+    if (!plan->identity) {  // slot-ordered results, gathered below
+        p.out_by_slot = 1;
+        p.out_slot_base = 0;
+        p.score = t_score;
+        p.end_i = sch.coords ? t_i : nullptr;
+        p.end_j = sch.coords ? t_j : nullptr;
+    }
     if (plan->multi) {
         p.group_lanes = 16;
         p.groups = 4;
         HIP_TRY(msw::launch_sw_multi(p, plan->table, sch.affine, sch.coords, st));
-        return MSW_OK;
+    } else {
+        p.n_slots = (uint32_t)plan->n;
+        p.lds_stride = msw::stream_stride(plan->max_n);
+        p.f16_ok = f16_fits(sch, plan->max_m, plan->max_n) ? 1u : 0u;
+        p.pairs_blocks = plan->single.pairs_blocks;
+        p.group_lanes = plan->single.group_lanes;
+        p.groups = plan->single.groups;
+        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, plan->max_m, plan->single.layout, st));
     }
-    p.n_slots = (uint32_t)plan->n;
-    p.lds_stride = msw::stream_stride(plan->max_n);
-    p.f16_ok = f16_fits(sch, plan->max_m, plan->max_n) ? 1u : 0u;
-    p.pairs_blocks = plan->single.pairs_blocks;
-    p.group_lanes = plan->single.group_lanes;
-    p.groups = plan->single.groups;
-    HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, plan->max_m, plan->single.layout, st));
+    if (!plan->identity)
+        HIP_TRY(msw::launch_gather_results(plan->d_inv, t_score, t_i, t_j, out->score, sch.coords ? out->end_i : nullptr,
+                                           sch.coords ? out->end_j : nullptr, n, st));
     return MSW_OK;
 }
 
 void msw_plan_destroy(msw_plan* plan) {
     if (!plan) return;
-    if (plan->d_order) {
+    if (plan->d_order || plan->d_inv || plan->d_tmp) {
         (void)hipSetDevice(plan->device);
-        (void)hipFree(plan->d_order);
+        for (void* q : {(void*)plan->d_order, (void*)plan->d_inv, (void*)plan->d_tmp})
+            if (q) (void)hipFree(q);
     }
     delete plan;
 }

@@ -65,6 +65,13 @@ DEF_KERNEL(k_add_f16, "v_add_f16 %0, %0, %1")
 DEF_KERNEL(k_maximum3_f32, "v_maximum3_f32 %0, %0, %1, %2")
 DEF_KERNEL(k_bfi, "v_bfi_b32 %0, %0, %1, %2")
 DEF_KERNEL(k_lshlrev, "v_lshlrev_b32 %0, 16, %0")
+// round 2: the cost of hazard wait states and of the wave_shr hand-off for a
+// lone wave (the config-2 loop has one DPP + s_nop 1 and ~4 s_nop 0 per step)
+DEF_KERNEL(k_pk_add_f16_nop0, "v_pk_add_f16 %0, %0, %1\n s_nop 0")
+DEF_KERNEL(k_pk_add_f16_nop1, "v_pk_add_f16 %0, %0, %1\n s_nop 1")
+DEF_KERNEL(k_and_wave_shr, "v_and_b32_dpp %0, %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+DEF_KERNEL(k_and_row_shr, "v_and_b32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+DEF_KERNEL(k_pk_max3_f16_clamp_pair, "v_pk_maximum3_f16 %0, %0, %1, %2\n v_pk_add_f16 %0, %1, %0 clamp")
 
 template <typename K>
 float run(K kern, int blocks, int threads, int iters, uint32_t* out) {
@@ -138,6 +145,11 @@ int main() {
     BENCH(k_maximum3_f32)
     BENCH(k_bfi)
     BENCH(k_lshlrev)
+    BENCH(k_pk_add_f16_nop0)
+    BENCH(k_pk_add_f16_nop1)
+    BENCH(k_and_wave_shr)
+    BENCH(k_and_row_shr)
+    BENCH(k_pk_max3_f16_clamp_pair)
     CHK(hipDeviceSynchronize());
     return 0;
 }
