@@ -75,7 +75,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-memory (PCIe) rate")
     ap.add_argument("--extra-configs", default="3,5",
-                    help="N = 1 only: other single-GPU configs timed as extra keys ('' = none)")
+                    help="N = 1 only: other single-GPU configs timed as extra keys ('' or 'none' = none)")
     ap.add_argument("--cpu-standin", action="store_true",
                     help="TEST ONLY (tests/test_bench_launcher.py): gloo ranks on the CPU with a "
                          "stand-in scorer, to exercise the launcher, sharding and gather without a GPU")
@@ -614,7 +614,7 @@ def main(argv=None):
             if not args.no_pcie:
                 pcie = pcie_rates(ctx, batch, scoring, cells, g_score)
                 cut = cut_roofline(ctx, dev, stream)
-            for c in [int(x) for x in args.extra_configs.split(",") if x.strip()]:
+            for c in [int(x) for x in args.extra_configs.split(",") if x.strip().isdigit()]:
                 if c != cfg:
                     extra[f"config{c}"] = time_extra_config(ctx, dev, stream, c, args)
         elif args.cpu_seconds > 0:

@@ -575,10 +575,21 @@ __device__ __forceinline__ uint32_t sel_round(const PairMeta& q, uint32_t* strea
 #ifndef MSW_EARLY_WIN_LOADS
 #define MSW_EARLY_WIN_LOADS 1
 #endif
-// Explicitly scheduled linear score-only f16 loop (see sw_body).
-#ifndef MSW_LIN_SCHED
-#define MSW_LIN_SCHED 1
+// Explicitly scheduled f16 loops of the pairs layout (see sw_body), per
+// scoring kind.  MI355X, tools/sched_ab.sh (10k pairs = one wave per SIMD /
+// 65k-200k pairs), explicit vs hipcc's schedule: linear 46.0 vs 48.1 us /
+// 227 vs 231 us, linear + coords 69.5 vs 77.2 / 347 vs 354, affine + coords
+// 102.9 vs 103.4 / 1585 vs 1594 (200k); affine score-only is faster with
+// hipcc's own schedule at 10k (81.1 vs 85.4, equal at 65k), so it keeps it.
+#ifndef MSW_EXPLICIT_SCHED
+#define MSW_EXPLICIT_SCHED 1
 #endif
+#ifndef MSW_EXPLICIT_AFF
+#define MSW_EXPLICIT_AFF 0
+#endif
+constexpr bool explicit_sched(bool affine, bool coords) {
+    return MSW_EXPLICIT_SCHED && (!affine || coords || MSW_EXPLICIT_AFF);
+}
 #ifndef MSW_PERM_LEAD_LIN
 #define MSW_PERM_LEAD_LIN 2
 #endif
@@ -657,7 +668,9 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
 #endif
     const int skew = SPLIT ? 2 * (G - 1) + 1 : G - 1;
     // wavefront steps, rounded up to a multiple of the steps per iteration
-    constexpr int kUnroll = step_unroll(AFFINE, COORDS);
+    // (the explicitly scheduled f16 loops of the pairs layout run four steps
+    // per iteration; an integer-path wave of the same kernel then rounds to four too)
+    constexpr int kUnroll = (!SPLIT && explicit_sched(AFFINE, COORDS)) ? 4 : step_unroll(AFFINE, COORDS);
     const int steps = (wave_max_nonneg(max(q.na, q.nb)) + skew + kUnroll - 1) & ~(kUnroll - 1);
     uint32_t* stream = lds + g * p.lds_stride;
 #if !MSW_EARLY_WIN_LOADS
@@ -735,23 +748,28 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
         uint32_t t1a[KR], t1b[KR];
         using P0 = std::integral_constant<int, 0>;
         using P1 = std::integral_constant<int, 1>;
-        if constexpr (F16 && !AFFINE && !COORDS && !SPLIT && MSW_LIN_SCHED) {
-            // Linear score-only f16 loop (configs 2 and 5), explicitly
-            // scheduled.  Every instruction is pinned by a sched_barrier so that
-            // each link of the row chain DPP -> clamp -> max3 -> clamp -> ...
-            // has exactly one independent instruction beside it: the
-            // substitution perm of the next row, the next step's diagonal add,
-            // or a score fold.  That keeps a lone wave (one per SIMD, config 2)
+        if constexpr (F16 && !SPLIT && explicit_sched(AFFINE, COORDS)) {
+            // The f16 loops of the pairs layout (every config's main kernel),
+            // explicitly scheduled.  Every instruction is pinned by a
+            // sched_barrier so that each link of the row chain -- linear:
+            // max3 -> clamp -> max3; affine: F = max(F_up - ge, G_up) -> max3 ->
+            // G = clamp(H - go - ge) -> next row's F -- has an independent
+            // instruction beside it: the substitution perm of the next row, the
+            // next step's diagonal add, the next row's E, a best-cell key or a
+            // score fold.  That keeps a lone wave (one per SIMD, config 2)
             // issuing without dependency stalls AND without the wait states
-            // hipcc otherwise inserts: an s_nop between a v_pk_maximum3_f16 and
-            // its immediate consumer (13 per four steps) and before the DPP
-            // hand-off (s_nop 1), which cost a lone wave ~3.8 / ~7.8 cycles
-            // each (tools/ubench_valu.hip, profiles/r02/ubench_valu_gfx950.txt).
-            // The next step's row-0 perm is issued in the last row's slot (it
-            // needs the word of step t+2, w2), and the score folds (rows
-            // 2k, 2k+1) run two rows later, the last pair at the next step's
-            // start, so the DPP reads the bottom row three instructions after
-            // it is written.
+            // hipcc otherwise inserts (an s_nop between a v_pk_maximum3_f16 and
+            // its immediate consumer, 13 per four linear steps, and an s_nop 1
+            // before the DPP hand-off), which cost a lone wave ~3.8 / ~7.8
+            // cycles each (tools/ubench_valu.hip, profiles/r02/ubench_valu_gfx950.txt);
+            // it also makes the loop immune to hipcc's register-pressure-driven
+            // rescheduling (affine + coordinates ran 96 or 104 us at 10k pairs
+            // depending on unrelated prologue code).  The next step's row-0
+            // perm is issued in the last row's slot (it needs the word of step
+            // t+2, w2); score folds (rows 2k, 2k+1) run two rows later, the
+            // last pair at the next step's start; the hand-offs (DPP) for the
+            // next step are issued at the end of this one, three or more
+            // instructions after the rows they read.
 #define MSW_SB __builtin_amdgcn_sched_barrier(0)
             {
                 const uint32_t w0 = wp[0];
@@ -760,21 +778,39 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
             }
             uint32_t an0 = sub(0, wp[1]);  // row 0's substitution at step 1's column
             uint32_t hpend = 0u, hkm2 = 0u;
-            // hu: the hand-off for the coming step (lane l-1's bottom row), issued
-            // at the end of the previous step -- three instructions after that
-            // row is written, and never first in the loop body, where hipcc
-            // would guard it with a wait state for the loop entry.
-            uint32_t hu = shr1_group(h_bot, top_mask);
-            auto sstep = [&](uint32_t w1, uint32_t w2, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR], auto parity)
-                             __attribute__((always_inline)) {
+            uint32_t hu = shr1_group(h_bot, top_mask);                  // H of the row above
+            uint32_t fu = AFFINE ? shr1_group(f_bot, top_mask) : 0u;   // F of the row above (affine)
+            auto sstep = [&](int t, uint32_t w1, uint32_t w2, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR],
+                             auto parity) __attribute__((always_inline)) {
                 constexpr int kParity = decltype(parity)::value;
-                uint32_t up = hadd_clamp(hu, nge);
-                MSW_SB;
-                t1n[0] = hadd(hu, an0);
-                MSW_SB;
-                // score fold left over from the previous step: odd KR pairs the
-                // last rows of two steps, even KR the previous step's last pair
-                if constexpr (KR & 1) {
+                // linear: up = E of the row above; affine: fsub = F_up - ge (the
+                // row's F needs G_up from the previous row's clamp), e_next = the
+                // next row's E = max(E_left - ge, G_left), both formed a row ahead
+                uint32_t up = 0u, g_up = 0u, e_next = 0u, fsub = 0u;
+                if constexpr (AFFINE) {
+                    fsub = hadd(fu, nge);
+                    MSW_SB;
+                    g_up = hadd_clamp(hu, noe);
+                    MSW_SB;
+                    const uint32_t el = hadd(E[0], nge);
+                    MSW_SB;
+                    t1n[0] = hadd(hu, an0);
+                    MSW_SB;
+                    e_next = hmax(el, GK[0]);
+                    MSW_SB;
+                } else {
+                    up = hadd_clamp(hu, nge);
+                    MSW_SB;
+                    t1n[0] = hadd(hu, an0);
+                    MSW_SB;
+                }
+                uint32_t nja = 0u;
+                if constexpr (COORDS) {
+                    nja = (nj_lane - (uint32_t)t) & 0xFFFFu;
+                    MSW_SB;
+                } else if constexpr (KR & 1) {
+                    // score fold left over from the previous step: odd KR pairs
+                    // the last rows of two steps, even KR the previous step's last pair
                     if constexpr (kParity == 0) {
                         best = track_max3(best, hpend, h_bot);
                         MSW_SB;
@@ -786,28 +822,88 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
                     MSW_SB;
                 }
                 uint32_t hh[KR];
+                // Best-cell keys of row r - 1 are formed during row r (two
+                // instructions) and folded into the running maxima a few slots
+                // later, so neither waits on a fresh value; the last row's after
+                // the loop.
+                uint32_t ka = 0u, kb = 0u;
+                auto key_form = [&](int r) __attribute__((always_inline)) {
+                    ka = (hh[r] << 16) | nja;
+                    MSW_SB;
+                    kb = (hh[r] & 0xFFFF0000u) | nja;
+                    MSW_SB;
+                };
+                auto key_fold = [&](int r) __attribute__((always_inline)) {
+                    key_a[r] = max(key_a[r], ka);
+                    MSW_SB;
+                    key_b[r] = max(key_b[r], kb);
+                    MSW_SB;
+                };
 #pragma unroll
                 for (int r = 0; r < KR; ++r) {
-                    const uint32_t h = pk_max3(t1[r], E[r], up);
-                    MSW_SB;
-                    uint32_t a = 0u;
-                    if (r + 1 < KR) a = sub(r + 1, w1);
-                    else an0 = sub(0, w2);
-                    MSW_SB;
-                    up = E[r] = hadd_clamp(h, nge);
-                    MSW_SB;
-                    if (r + 1 < KR) {
+                    const bool last = r + 1 == KR;
+                    uint32_t h, a = 0u;
+                    if constexpr (AFFINE) {
+                        // F -> [el, perm] -> h -> [fsub, e_next, keys r-1] -> G -> [t1n, keys r-1] -> next F
+                        const uint32_t e = e_next;
+                        const uint32_t F = hmax(fsub, g_up);                // [chain]
+                        MSW_SB;
+                        uint32_t el = 0u;
+                        if (!last) {
+                            el = hadd(E[r + 1], nge);
+                            MSW_SB;
+                            a = sub(r + 1, w1);
+                        } else {
+                            an0 = sub(0, w2);
+                        }
+                        MSW_SB;
+                        h = pk_max3(t1[r], e, F);                           // [chain]
+                        MSW_SB;
+                        hh[r] = h;
+                        E[r] = e;
+                        if (!last) fsub = hadd(F, nge);
+                        else fu = shr1_group(F, top_mask);                  // next step's F hand-off
+                        MSW_SB;
+                        if (!last) {
+                            e_next = hmax(el, GK[r + 1]);
+                            MSW_SB;
+                        }
+                        if constexpr (COORDS) {
+                            if (r > 0) key_form(r - 1);
+                        }
+                        g_up = GK[r] = hadd_clamp(h, noe);                  // [chain]
+                        MSW_SB;
+                    } else {
+                        // h -> [perm, keys r-1] -> E -> [t1n, keys r-1] -> next h
+                        h = pk_max3(t1[r], E[r], up);                       // [chain]
+                        MSW_SB;
+                        hh[r] = h;
+                        if (!last) a = sub(r + 1, w1);
+                        else an0 = sub(0, w2);
+                        MSW_SB;
+                        if constexpr (COORDS) {
+                            if (r > 0) key_form(r - 1);
+                        }
+                        up = E[r] = hadd_clamp(h, nge);                     // [chain]
+                        MSW_SB;
+                    }
+                    if (!last) {
                         t1n[r + 1] = hadd(h, a);
                         MSW_SB;
                     }
-                    hh[r] = h;
-                    if (r >= 2 && (r & 1) == 0) {
+                    if constexpr (COORDS) {
+                        if (r > 0) key_fold(r - 1);
+                    } else if (r >= 2 && (r & 1) == 0) {
                         best = track_max3(best, hh[r - 2], hh[r - 1]);
                         MSW_SB;
                     }
                 }
+                if constexpr (COORDS) {
+                    key_form(KR - 1);
+                    key_fold(KR - 1);
+                }
                 h_bot = hh[KR - 1];
-                if constexpr ((KR & 1) == 0) hkm2 = hh[KR - 2];
+                if constexpr (!COORDS && (KR & 1) == 0) hkm2 = hh[KR - 2];
                 hu = shr1_group(h_bot, top_mask);
                 MSW_SB;
             };
@@ -817,17 +913,17 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
             for (int t = 0; t < steps; t += 4) {
                 const uint32_t base = lds_wp + 4u * (uint32_t)t;
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wb));
-                sstep(wa.x, wa.y, t1a, t1b, P0{});
-                sstep(wa.y, wb.x, t1b, t1a, P1{});
+                sstep(t, wa.x, wa.y, t1a, t1b, P0{});
+                sstep(t + 1, wa.y, wb.x, t1b, t1a, P1{});
                 asm volatile("ds_read2_b32 %0, %1 offset0:5 offset1:6" : "=v"(wa) : "v"(base));
-                sstep(wb.x, wb.y, t1a, t1b, P0{});
+                sstep(t + 2, wb.x, wb.y, t1a, t1b, P0{});
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wa));
-                sstep(wb.y, wa.x, t1b, t1a, P1{});
+                sstep(t + 3, wb.y, wa.x, t1b, t1a, P1{});
                 asm volatile("ds_read2_b32 %0, %1 offset0:7 offset1:8" : "=v"(wb) : "v"(base));
             }
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wb));
-            // the pair still pending after the last (odd) step
-            best = track_max3(best, (KR & 1) ? hpend : hkm2, h_bot);
+            // the score pair still pending after the last (odd) step
+            if constexpr (!COORDS) best = track_max3(best, (KR & 1) ? hpend : hkm2, h_bot);
 #undef MSW_SB
             return;
         }

@@ -15,7 +15,7 @@ for CFG in 2 3 5; do
     3) ARGS="--steps 5 --warmup 2" ;;
     5) ARGS="--steps 20 --warmup 3" ;;
   esac
-  BENCH="python3 bench.py --config $CFG $ARGS --cpu-seconds 0 --no-pcie"
+  BENCH="python3 bench.py --config $CFG $ARGS --cpu-seconds 0 --no-pcie --extra-configs none"
   D="$OUT/c$CFG"
   mkdir -p "$D"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$D/trace" -o t --output-format csv -- $BENCH > "$D/trace.log" 2>&1

@@ -73,6 +73,34 @@ DEF_KERNEL(k_and_wave_shr, "v_and_b32_dpp %0, %0, %1 wave_shr:1 row_mask:0xf ban
 DEF_KERNEL(k_and_row_shr, "v_and_b32_dpp %0, %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
 DEF_KERNEL(k_pk_max3_f16_clamp_pair, "v_pk_maximum3_f16 %0, %0, %1, %2\n v_pk_add_f16 %0, %1, %0 clamp")
 
+// Two independent chains per asm statement (v, w), 8 of each: the issue rate
+// of a lone wave when two instruction types alternate (pipe co-issue).
+#define DEF_MIX(NAME, ASM)                                                              \
+template <int CHAINS>                                                                  \
+__global__ void NAME(uint32_t* out, int iters, uint32_t seed) {                       \
+    uint32_t v[8], w[8];                                                               \
+    for (int k = 0; k < 8; ++k) { v[k] = seed * (threadIdx.x + k + 1); w[k] = v[k] ^ 0x55u; } \
+    uint32_t b = seed ^ 0x1234u, c = seed ^ 0x777u;                                    \
+    for (int i = 0; i < iters; ++i) {                                                  \
+        _Pragma("unroll")                                                              \
+        for (int r = 0; r < 8; ++r) {                                                  \
+            _Pragma("unroll")                                                          \
+            for (int k = 0; k < CHAINS; ++k) asm volatile(ASM : "+v"(v[k]), "+v"(w[k]) : "v"(b), "v"(c)); \
+        }                                                                              \
+    }                                                                                  \
+    uint32_t s = 0;                                                                    \
+    for (int k = 0; k < CHAINS; ++k) s ^= v[k] ^ w[k];                                 \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                    \
+}
+DEF_MIX(m_pkadd_pkadd, "v_pk_add_f16 %0, %0, %2\n v_pk_add_f16 %1, %1, %3")
+DEF_MIX(m_pkadd_lshlor, "v_pk_add_f16 %0, %0, %2\n v_lshl_or_b32 %1, %1, 16, %3")
+DEF_MIX(m_pkadd_perm, "v_pk_add_f16 %0, %0, %2\n v_perm_b32 %1, %1, %2, %3")
+DEF_MIX(m_pkmax3_max3u, "v_pk_maximum3_f16 %0, %0, %2, %3\n v_max3_u32 %1, %1, %2, %3")
+DEF_MIX(m_pkadd_xor, "v_pk_add_f16 %0, %0, %2\n v_xor_b32 %1, %1, %3")
+DEF_MIX(m_pkadd_addu32, "v_pk_add_f16 %0, %0, %2\n v_add_u32 %1, %1, %3")
+DEF_MIX(m_perm_perm, "v_perm_b32 %0, %0, %2, %3\n v_perm_b32 %1, %1, %2, %3")
+DEF_MIX(m_lshlor_bfi, "v_lshl_or_b32 %0, %0, 16, %2\n v_bfi_b32 %1, %1, %2, %3")
+
 template <typename K>
 float run(K kern, int blocks, int threads, int iters, uint32_t* out) {
     hipEvent_t a, b;
@@ -100,6 +128,17 @@ float run(K kern, int blocks, int threads, int iters, uint32_t* out) {
         printf("%-16s full-ILP8 %.2f cyc/instr/SIMD | full-1chain %.2f | 1wave chain %.2f cyc/instr | 1wave ILP8 %.2f\n", \
                #NAME, t8 * 1e-3 * 2.4e9 * 1024 / ops8, t1 * 1e-3 * 2.4e9 * 1024 / ops1,              \
                l1 * 1e-3 * 2.4e9 * 1024 / lat_ops, i8 * 1e-3 * 2.4e9 * 1024 / (lat_ops * 8));        \
+    }
+
+#define BENCH_MIX(NAME)                                                                               \
+    {                                                                                                 \
+        const int iters = 4096;                                                                       \
+        float i8 = run(NAME<8>, 256 * 4, 64, iters, out);    /* 1 wave/SIMD, 2 x 8 chains */          \
+        float f8 = run(NAME<8>, 256 * 16, 256, iters, out);  /* 16 waves/SIMD */                      \
+        double lat_ops = 256.0 * 4 * iters * 8 * 8 * 2;                                               \
+        double ops8 = 256.0 * 16 * 256 / 64 * iters * 8 * 8 * 2;                                      \
+        printf("%-16s mix: 1wave %.2f cyc/instr | full %.2f cyc/instr/SIMD\n", #NAME,                   \
+               i8 * 1e-3 * 2.4e9 * 1024 / lat_ops, f8 * 1e-3 * 2.4e9 * 1024 / ops8);                  \
     }
 
 int main() {
@@ -150,6 +189,14 @@ int main() {
     BENCH(k_and_wave_shr)
     BENCH(k_and_row_shr)
     BENCH(k_pk_max3_f16_clamp_pair)
+    BENCH_MIX(m_pkadd_pkadd)
+    BENCH_MIX(m_pkadd_lshlor)
+    BENCH_MIX(m_pkadd_perm)
+    BENCH_MIX(m_pkmax3_max3u)
+    BENCH_MIX(m_pkadd_xor)
+    BENCH_MIX(m_pkadd_addu32)
+    BENCH_MIX(m_perm_perm)
+    BENCH_MIX(m_lshlor_bfi)
     CHK(hipDeviceSynchronize());
     return 0;
 }

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--reads-per-file", type=int, default=1_000_000)
     ap.add_argument("--genome-bases", type=int, default=64 << 20)
     ap.add_argument("--readers", default="16")
+    ap.add_argument("--host-threads", default="",
+                    help="comma list of MSW_HOST_THREADS values to sweep (readers then default to it); "
+                         "overrides --readers")
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--out", default="gpurun_out/wgs_e2e.jsonl")
@@ -45,11 +48,18 @@ def main():
     print(f"dataset: {len(ds['files'])} files, {gz_bytes / 1e6:.0f} MB gz, written in {gen_s:.1f} s", flush=True)
     cli = os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini")
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
-    for readers in [int(x) for x in args.readers.split(",")]:
-        rec = os.path.join(args.dir, f"rec_{readers}.json")
+    sweep = ([("threads", int(x)) for x in args.host_threads.split(",")] if args.host_threads
+             else [("readers", int(x)) for x in args.readers.split(",")])
+    for kind, readers in sweep:
+        rec = os.path.join(args.dir, f"rec_{kind}_{readers}.json")
         env = dict(os.environ, WGS_DATA_DIR=args.dir, WGS_SAMPLE_ID="SYN", WGS_LANES=str(args.lanes),
                    WGS_READS_PER_LANE=str(args.reads_per_lane), GPU_CHUNK_SIZE_READS=str(args.chunk),
-                   WGS_RUN_ID=f"e2e_{readers}_{int(time.time())}", MSW_READERS=str(readers))
+                   WGS_RUN_ID=f"e2e_{kind}_{readers}_{int(time.time())}")
+        if kind == "threads":
+            env["MSW_HOST_THREADS"] = str(readers)
+            env.pop("MSW_READERS", None)
+        else:
+            env["MSW_READERS"] = str(readers)
         for kv in filter(None, args.extra_env.split(",")):
             k, v = kv.split("=", 1)
             env[k] = v
@@ -62,7 +72,7 @@ def main():
             print(r.stdout[-3000:], r.stderr[-3000:])
             raise SystemExit(f"CLI failed with {r.returncode}")
         d = json.load(open(rec))
-        d.update({"readers": readers, "process_wall_s": round(wall, 3), "gz_bytes": gz_bytes,
+        d.update({"sweep": kind, kind: readers, "process_wall_s": round(wall, 3), "gz_bytes": gz_bytes,
                   "chunk_reads": args.chunk, "extra_env": args.extra_env, "bgzf": args.bgzf,
                   "dataset": f"{args.lanes} lanes x {args.reads_per_lane} files x {args.reads_per_file} "
                              f"150 bp reads, {args.genome_bases} bp genome, window 300"})
