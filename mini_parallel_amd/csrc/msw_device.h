@@ -149,8 +149,20 @@ __device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t
     // contiguous and the host / a gather pass restores pair order.
     q.oa = p.out_by_slot ? p.out_slot_base + sa : q.pa;
     q.ob = p.out_by_slot ? p.out_slot_base + sb : q.pb;
-    const int ma = p.read_len[q.pa], na = p.win_len[q.pa];
-    const int mb = SPLIT ? ma : (int)p.read_len[q.pb], nb = SPLIT ? na : (int)p.win_len[q.pb];
+    int ma, na, mb, nb;
+    if (p.slot_lens) {  // lengths in slot order (planned batches): contiguous, not gathered
+        const uint32_t la = p.slot_lens[p.out_slot_base + sa];
+        const uint32_t lb = SPLIT ? la : p.slot_lens[p.out_slot_base + sb];
+        ma = (int)(la & 0xFFFFu);
+        na = (int)(la >> 16);
+        mb = (int)(lb & 0xFFFFu);
+        nb = (int)(lb >> 16);
+    } else {
+        ma = p.read_len[q.pa];
+        na = p.win_len[q.pa];
+        mb = SPLIT ? ma : (int)p.read_len[q.pb];
+        nb = SPLIT ? na : (int)p.win_len[q.pb];
+    }
     q.ma = q.va ? ma : 0;
     q.mb = q.vb ? mb : 0;
     q.na = q.va ? na : 0;
@@ -489,7 +501,10 @@ __device__ __forceinline__ void load_round(const SwParams& p, uint32_t pa, uint3
                                            WinRound& w) {
     const uint8_t* wa = p.wins + (uint64_t)pa * p.win_stride;
     const uint8_t* wb = p.wins + (uint64_t)pb * p.win_stride;
-    const int top = (int)(p.win_stride >> 4) - 1;  // last loadable chunk
+    // last chunk to load: the row's end or the stream's (the launch's longest
+    // window), whichever comes first -- lanes past it re-load that chunk (the
+    // same line, coalesced) instead of touching a line past the windows
+    const int top = min((int)(p.win_stride >> 4), (int)((p.lds_stride - kLead) >> 4)) - 1;
     const int last = (int)p.win_stride - 1;
 #pragma unroll
     for (int u = 0; u < kRound; ++u) {

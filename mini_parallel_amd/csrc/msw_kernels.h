@@ -63,6 +63,10 @@ struct SwParams {
     // pair order (msw_runtime.cpp: the host drain, or launch_gather_results).
     uint32_t out_by_slot;
     uint32_t out_slot_base;
+    // Optional lengths in slot order, read_len | win_len << 16 per slot (index
+    // out_slot_base + slot): planned batches read them contiguously instead of
+    // gathering two 2-byte lengths per pair through the order array.
+    const uint32_t* slot_lens;
 };
 
 // f16 bits of the cell value v * 2^-11 (|v| < 2048: exact, normal or zero).
@@ -88,7 +92,7 @@ __host__ __device__ inline uint32_t pairs_per_wave(bool split, uint32_t groups) 
 
 // 16-byte vector loads of the window rows are legal.
 inline uint32_t vec_ok(const void* base, uint64_t stride) {
-    return (stride % 16 == 0 && ((uintptr_t)base & 15) == 0) ? 1u : 0u;
+    return (stride >= 16 && stride % 16 == 0 && ((uintptr_t)base & 15) == 0) ? 1u : 0u;
 }
 
 // Dynamic LDS bytes for one 64-lane block (one window stream per group).

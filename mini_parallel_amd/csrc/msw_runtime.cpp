@@ -1055,6 +1055,7 @@ struct msw_plan {
     bool identity = true;
     uint32_t* d_inv = nullptr;
     uint8_t* d_tmp = nullptr;
+    uint32_t* d_slot_lens = nullptr;  // read_len | win_len << 16 in slot order
     bool multi = false;
     msw::MultiTable table{};
     LaunchPlan single{};
@@ -1098,10 +1099,16 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
         if (!rc && e != hipSuccess) rc = fail(MSW_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
         for (uint64_t k = 0; k < n_pairs && pl->identity; ++k) pl->identity = order[k] == (uint32_t)k;
         if (!rc && !pl->identity) {
-            std::vector<uint32_t> inv(n_pairs);
-            for (uint64_t k = 0; k < n_pairs; ++k) inv[order[k]] = (uint32_t)k;
-            if (!(rc = grow_dev(&pl->d_inv, n_pairs)) && !(rc = grow_dev(&pl->d_tmp, n_pairs * kResBytesPerPair))) {
+            std::vector<uint32_t> inv(n_pairs), lens(n_pairs);
+            for (uint64_t k = 0; k < n_pairs; ++k) {
+                inv[order[k]] = (uint32_t)k;
+                lens[k] = (uint32_t)read_len[order[k]] | ((uint32_t)win_len[order[k]] << 16);
+            }
+            if (!(rc = grow_dev(&pl->d_inv, n_pairs)) && !(rc = grow_dev(&pl->d_tmp, n_pairs * kResBytesPerPair)) &&
+                !(rc = grow_dev(&pl->d_slot_lens, n_pairs))) {
                 e = hipMemcpy(pl->d_inv, inv.data(), n_pairs * sizeof(uint32_t), hipMemcpyHostToDevice);
+                if (e == hipSuccess)
+                    e = hipMemcpy(pl->d_slot_lens, lens.data(), n_pairs * sizeof(uint32_t), hipMemcpyHostToDevice);
                 if (e != hipSuccess) rc = fail(MSW_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
             }
         }
@@ -1145,9 +1152,10 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
     int32_t* t_score = reinterpret_cast<int32_t*>(plan->d_tmp);
     int16_t* t_i = reinterpret_cast<int16_t*>(plan->d_tmp + 4 * n);
     int16_t* t_j = reinterpret_cast<int16_t*>(plan->d_tmp + 6 * n);
-    if (!plan->identity) {  // slot-ordered results, gathered below
+    if (!plan->identity) {  // slot-ordered lengths and results, gathered below
         p.out_by_slot = 1;
         p.out_slot_base = 0;
+        p.slot_lens = plan->d_slot_lens;
         p.score = t_score;
         p.end_i = sch.coords ? t_i : nullptr;
         p.end_j = sch.coords ? t_j : nullptr;
@@ -1173,9 +1181,9 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
 
 void msw_plan_destroy(msw_plan* plan) {
     if (!plan) return;
-    if (plan->d_order || plan->d_inv || plan->d_tmp) {
+    if (plan->d_order || plan->d_inv || plan->d_tmp || plan->d_slot_lens) {
         (void)hipSetDevice(plan->device);
-        for (void* q : {(void*)plan->d_order, (void*)plan->d_inv, (void*)plan->d_tmp})
+        for (void* q : {(void*)plan->d_order, (void*)plan->d_inv, (void*)plan->d_tmp, (void*)plan->d_slot_lens})
             if (q) (void)hipFree(q);
     }
     delete plan;
