@@ -198,18 +198,35 @@ int msw_align_reads(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g, 
 int msw_align_reads_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g,
                           const msw_read_batch_t* batch, msw_out_t* out, uint64_t chunk_pairs, uint64_t* ticket);
 
+/* Device-resident reads against genome windows (the GPU lane reader's
+ * batches, msw_gfastq_next): read p = reads[p * read_stride ..][0,
+ * read_len[p]) scores against genome[win_pos[p], win_pos[p] + W), W = window,
+ * or 2 x read_len[p] when window is 0 (the CLI's --window rule), capped at
+ * 4096 and clipped at the genome end.  Windows are cut into a context scratch
+ * slab on the GPU; everything is enqueued on `stream` (NULL = the context's
+ * compute stream), no host synchronisation.  All arrays are device memory;
+ * win_len_out (may be NULL) receives the clipped window lengths.
+ * max_read_len bounds read_len (it selects the kernel instance). */
+int msw_align_reads_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g, const uint8_t* reads,
+                           const uint16_t* read_len, uint32_t read_stride, const int64_t* win_pos, uint64_t n,
+                           uint32_t window, uint32_t max_read_len, msw_out_t* out, uint16_t* win_len_out,
+                           void* stream);
+
 /* Device memory helpers for callers that keep batches resident in HBM. */
 void* msw_dev_alloc(msw_ctx* ctx, size_t bytes);
 void msw_dev_free(msw_ctx* ctx, void* p);
 int msw_memcpy_h2d(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
 int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* enqueued on `stream` (NULL = the context's compute stream); dst should be pinned */
+int msw_memcpy_d2h_async(msw_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
 int msw_synchronize(msw_ctx* ctx);
 
 /* Counters of the host-batch calls (msw_align_batch*, msw_align_reads*) on a
  * context, for run records (the reference's BenchmarkResult,
  * tools/benchmark.rs:17-34, reports only wall-clock rates):
  * kernel_ms = GPU time of the scoring launches (HIP events on the compute
- * stream around each chunk's launch, added when the chunk is drained),
+ * stream around each chunk's launch, added when the chunk is drained; and
+ * of msw_align_reads_device launches, added when they have finished),
  * alg_bytes = read + window bytes + 4 B score (+ 4 B coordinates) per pair,
  * the kernel's algorithmic HBM traffic.  reset != 0 zeroes them after the copy. */
 typedef struct {

@@ -20,6 +20,8 @@
 
 #include <stdint.h>
 
+#include "msw.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -52,6 +54,53 @@ void msw_fastq_stats(const msw_fastq* fq, uint64_t* lines, uint64_t* reads, uint
 
 /* count_bases_in_fastq (aligner.rs:535-544): total bases and reads. */
 int msw_fastq_count_bases(const char* path, uint64_t* bases, uint64_t* reads);
+
+/* ------------------------------------------------------------------------
+ * GPU-side lane reader for BGZF files (the --full-wgs hot path's caller).
+ * The host reads compressed bytes only; inflate (RFC 1951), the CRC-32 check,
+ * the line split / UTF-8 / record numbering above and the sequence copy run
+ * on the GPU, and the reads land in HBM in the slab layout the scoring
+ * entry points take (msw_align_batch_device, msw_genome_cut_device).  Same
+ * semantics and error messages as msw_fastq_next; same reads in the same
+ * order.  Replaces process_fastq_file_in_chunks (aligner.rs:107-178) for
+ * BGZF lane files (a plain gzip member is MSW_E_INVALID: use msw_fastq_*).
+ * ------------------------------------------------------------------------ */
+typedef struct msw_gfastq msw_gfastq;
+
+typedef struct {
+    const uint8_t* reads;      /* device: reads[n][read_stride], zero-padded */
+    const uint16_t* read_len;  /* device */
+    const int64_t* pos;        /* device, or NULL unless opened with want_pos: pos= of the header, -1 */
+    uint32_t read_stride;
+    uint64_t n;                /* reads in this batch; 0 = end of file */
+    uint64_t first_read;       /* file index of the batch's first read */
+    uint32_t min_len, max_len; /* bounds over the span the batch comes from */
+} msw_dev_reads_t;
+
+/* is path a BGZF file (first member has the 'BC' extra field)? 1 / 0 */
+int msw_is_bgzf(const char* path);
+
+/* read_stride: multiple of 16, <= 256 (longer sequences are MSW_E_RANGE);
+ * max_reads: batch size (device slabs for two batches are allocated);
+ * span_bytes: decompressed bytes inflated and parsed per step (0 = default
+ * 256 MiB, env MSW_GFASTQ_SPAN_MB). */
+int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64_t max_reads, int want_pos,
+                    uint64_t span_bytes, msw_gfastq** out);
+/* The next batch, enqueued on `stream` (a hipStream_t; NULL = the context's
+ * compute stream) -- scoring launched after it on that stream sees it.  The
+ * device arrays stay valid until the call after next (two slabs alternate). */
+int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out);
+/* lines (valid), reads, errors (invalid lines), bases, compressed and inflated bytes so far */
+void msw_gfastq_stats(const msw_gfastq* g, uint64_t* lines, uint64_t* reads, uint64_t* errors, uint64_t* bases,
+                      uint64_t* bytes_in, uint64_t* bytes_out);
+void msw_gfastq_close(msw_gfastq* g);
+
+/* Host-to-host BGZF inflate on the GPU (test / tool form of the same
+ * kernels): data[0, len) is a whole BGZF file; out receives the
+ * decompressed bytes (*out_len).  MSW_E_INVALID on bad data (message names
+ * the member and the error), MSW_E_RANGE if cap is too small. */
+int msw_bgzf_inflate(msw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t* out, uint64_t cap,
+                     uint64_t* out_len);
 
 #ifdef __cplusplus
 }

@@ -28,11 +28,13 @@ EXPORTED = (
     "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
     "msw_plan_create", "msw_align_batch_planned", "msw_plan_destroy",
     "msw_genome_create", "msw_genome_destroy", "msw_genome_length", "msw_align_reads",
-    "msw_align_reads_async", "msw_genome_cut_device", "msw_ctx_stats",
+    "msw_align_reads_async", "msw_genome_cut_device", "msw_ctx_stats", "msw_align_reads_device",
+    "msw_memcpy_d2h_async",
 )
 # include/msw_fastq.h
 FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_next_packed",
-                  "msw_fastq_stats", "msw_fastq_count_bases")
+                  "msw_fastq_stats", "msw_fastq_count_bases", "msw_is_bgzf", "msw_gfastq_open",
+                  "msw_gfastq_next", "msw_gfastq_stats", "msw_gfastq_close", "msw_bgzf_inflate")
 
 
 class MswError(RuntimeError):
@@ -65,6 +67,12 @@ class ReadBatchT(ctypes.Structure):
 class OutT(ctypes.Structure):
     _fields_ = [("score", ctypes.c_void_p), ("end_i", ctypes.c_void_p),
                 ("end_j", ctypes.c_void_p)]
+
+
+class DevReadsT(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_void_p), ("read_len", ctypes.c_void_p), ("pos", ctypes.c_void_p),
+                ("read_stride", ctypes.c_uint32), ("n", ctypes.c_uint64), ("first_read", ctypes.c_uint64),
+                ("min_len", ctypes.c_uint32), ("max_len", ctypes.c_uint32)]
 
 
 class DeviceInfoT(ctypes.Structure):
@@ -109,6 +117,8 @@ def _declare(L):
         "msw_align_reads_async": (I, [P, ctypes.POINTER(ScoringT), P, ctypes.POINTER(ReadBatchT),
                                       ctypes.POINTER(OutT), ctypes.c_uint64,
                                       ctypes.POINTER(ctypes.c_uint64)]),
+        "msw_align_reads_device": (I, [P, ctypes.POINTER(ScoringT), P, P, P, ctypes.c_uint32, P, ctypes.c_uint64,
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(OutT), P, P]),
         "msw_align_compat": (I, [P, P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.c_uint32,
                                  ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]),
         "msw_host_alloc": (P, [ctypes.c_size_t]),
@@ -117,6 +127,7 @@ def _declare(L):
         "msw_dev_free": (None, [P, P]),
         "msw_memcpy_h2d": (I, [P, P, ctypes.c_size_t]),
         "msw_memcpy_d2h": (I, [P, P, ctypes.c_size_t]),
+        "msw_memcpy_d2h_async": (I, [P, P, P, ctypes.c_size_t, P]),
         "msw_synchronize": (I, [P]),
         "msw_ctx_stats": (I, [P, ctypes.POINTER(StatsT), I]),
         "msw_last_error": (ctypes.c_char_p, []),
@@ -131,6 +142,13 @@ def _declare(L):
                                    ctypes.POINTER(ctypes.c_uint64)]),
         "msw_fastq_count_bases": (I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(ctypes.c_uint64)]),
+        "msw_is_bgzf": (I, [ctypes.c_char_p]),
+        "msw_gfastq_open": (I, [P, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64, I, ctypes.c_uint64,
+                                ctypes.POINTER(P)]),
+        "msw_gfastq_next": (I, [P, P, ctypes.POINTER(DevReadsT)]),
+        "msw_gfastq_stats": (None, [P] + [ctypes.POINTER(ctypes.c_uint64)] * 6),
+        "msw_gfastq_close": (None, [P]),
+        "msw_bgzf_inflate": (I, [P, P, ctypes.c_uint64, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

@@ -504,6 +504,8 @@ struct WgsReport {
     int readers = 0;
     int host_threads = 0;
     std::vector<msw_stats_t> gpu;  // per worker: kernel time and algorithmic bytes (msw_ctx_stats)
+    bool gpu_inflate = false;      // lane files inflated and parsed on the GPUs
+    unsigned long long gz_in = 0, gz_out = 0;  // compressed / inflated bytes (GPU lane reader)
 };
 
 // GPU contexts of the --full-wgs workers: --num-gpus N of the visible devices,
@@ -588,6 +590,181 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                c.score, c.total_reads, c.total_bases, f.ms / 1000.0, c.completed ? "" : " (FAILED)");
         fflush(stdout);
     };
+
+    // GPU lane reader (sw mode, every lane file BGZF, MSW_GPU_INFLATE != 0):
+    // each worker takes whole files; the host reads compressed bytes only and
+    // inflate, parse, window cut and scoring run on the worker's GPU
+    // (msw_gfastq_* + msw_align_reads_device).  Per-read results come back to
+    // the host for the i64 sums and --scores-out, one batch behind the GPU.
+    bool gpu_reader = sw && env_or("MSW_GPU_INFLATE", "1") != "0" && !todo.empty();
+    for (size_t fi : todo) gpu_reader = gpu_reader && msw_is_bgzf(files[fi].c_str());
+    if (gpu_reader) {
+        std::atomic<unsigned long long> gz_in{0}, gz_out{0};
+        const uint64_t batch = std::max<uint64_t>(
+            chunk, strtoull(env_or("MSW_GFASTQ_BATCH", std::to_string(1u << 20)).c_str(), nullptr, 10));
+        std::atomic<size_t> next_file{0};
+        std::vector<std::thread> workers;
+        for (int gi = 0; gi < ngpu; ++gi) {
+            workers.emplace_back([&, gi]() {
+                Ctx ctx(devices[gi].ordinal);
+                const msw_scoring_t sc = scoring_of(a);
+                msw_genome* gen = nullptr;
+                if (msw_genome_create(ctx.h, (const uint8_t*)genome.data(), genome.size(), &gen) != MSW_OK)
+                    die(std::string("GPU genome upload error: ") + msw_last_error());
+                // two result sets: batch k's copy-back lands while batch k+1 runs
+                struct Res {
+                    int32_t* d_score = nullptr;
+                    int16_t *d_ei = nullptr, *d_ej = nullptr;
+                    uint16_t* d_wlen = nullptr;
+                    uint8_t* h = nullptr;  // pinned: score i32 | ei i16 | ej i16 | rlen u16 | wlen u16
+                    uint64_t n = 0, first = 0;
+                    size_t fi = 0;
+                    bool live = false;
+                } res[2];
+                const size_t rec = 4 + 2 + 2 + 2 + 2;
+                for (Res& r : res) {
+                    r.d_score = (int32_t*)msw_dev_alloc(ctx.h, batch * 4);
+                    r.d_ei = (int16_t*)msw_dev_alloc(ctx.h, batch * 2);
+                    r.d_ej = (int16_t*)msw_dev_alloc(ctx.h, batch * 2);
+                    r.d_wlen = (uint16_t*)msw_dev_alloc(ctx.h, batch * 2);
+                    r.h = (uint8_t*)msw_host_alloc(batch * rec);
+                    if (!r.d_score || !r.d_ei || !r.d_ej || !r.d_wlen || !r.h)
+                        die(std::string("GPU lane reader buffers: ") + msw_last_error());
+                }
+                unsigned long long alg_local = 0;
+                // host side of a finished batch: sums, cells, per-read records
+                auto settle = [&](Res& r) {
+                    if (!r.live) return;
+                    r.live = false;
+                    FileState& f = *st[r.fi];
+                    if (msw_synchronize(ctx.h) != MSW_OK) {
+                        fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
+                        f.failed = true;
+                        return;
+                    }
+                    const int32_t* sc32 = (const int32_t*)r.h;
+                    const int16_t* ei = (const int16_t*)(r.h + batch * 4);
+                    const int16_t* ej = ei + batch;
+                    const uint16_t* rl = (const uint16_t*)(ej + batch);
+                    const uint16_t* wl = rl + batch;
+                    long long sum = 0;
+                    unsigned long long cl = 0, nb = 0, nw = 0;
+                    for (uint64_t i = 0; i < r.n; ++i) {
+                        sum += sc32[i];
+                        cl += (unsigned long long)rl[i] * wl[i];
+                        nb += rl[i];
+                        nw += wl[i];
+                    }
+                    alg_local += nb + nw + (sc.want_coords ? 8ull : 4ull) * r.n;
+                    f.score += sum;
+                    f.bases += nb;
+                    f.reads += r.n;
+                    cells += cl;
+                    if (f.scores_fd >= 0) {
+                        std::vector<uint8_t> out(r.n * 8);
+                        for (uint64_t i = 0; i < r.n; ++i) {
+                            memcpy(&out[i * 8], &sc32[i], 4);
+                            memcpy(&out[i * 8 + 4], &ei[i], 2);
+                            memcpy(&out[i * 8 + 6], &ej[i], 2);
+                        }
+                        if (pwrite(f.scores_fd, out.data(), out.size(), (off_t)(r.first * 8)) != (ssize_t)out.size()) {
+                            fprintf(stderr, "  error writing scores for %s\n", f.path.c_str());
+                            f.failed = true;
+                        }
+                    }
+                };
+                int cur = 0;
+                for (;;) {
+                    const size_t k = next_file.fetch_add(1);
+                    if (k >= todo.size()) break;
+                    const size_t fi = todo[k];
+                    FileState& f = *st[fi];
+                    f.t0 = Clock::now();
+                    if (!a.scores_out.empty()) {
+                        const size_t slash = f.path.find_last_of('/');
+                        const std::string out = a.scores_out + "/" +
+                                                (slash == std::string::npos ? f.path : f.path.substr(slash + 1)) +
+                                                ".scores";
+                        f.scores_fd = open(out.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+                        if (f.scores_fd < 0) die("error: cannot create " + out);
+                    }
+                    printf("  Processing file %zu/%zu: %s (GPU inflate)\n", fi + 1, files.size(), f.path.c_str());
+                    fflush(stdout);
+                    msw_gfastq* gr = nullptr;
+                    if (msw_gfastq_open(ctx.h, f.path.c_str(), kReadStride, batch, 1, 0, &gr) != MSW_OK) {
+                        f.error = msw_last_error();
+                        fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
+                        f.failed = true;
+                    }
+                    while (gr) {
+                        msw_dev_reads_t d;
+                        if (msw_gfastq_next(gr, nullptr, &d) != MSW_OK) {
+                            f.error = msw_last_error();
+                            fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
+                            f.failed = true;
+                            break;
+                        }
+                        if (d.n == 0) break;
+                        Res& r = res[cur];
+                        settle(r);  // the batch before last used this result set
+                        msw_out_t o{r.d_score, r.d_ei, r.d_ej};
+                        if (msw_align_reads_device(ctx.h, &sc, gen, d.reads, d.read_len, d.read_stride, d.pos, d.n,
+                                                   a.window > 0 ? (uint32_t)a.window : 0u, d.max_len, &o, r.d_wlen,
+                                                   nullptr) != MSW_OK ||
+                            msw_memcpy_d2h_async(ctx.h, r.h, r.d_score, d.n * 4, nullptr) != MSW_OK ||
+                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 4, r.d_ei, d.n * 2, nullptr) != MSW_OK ||
+                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 6, r.d_ej, d.n * 2, nullptr) != MSW_OK ||
+                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 8, d.read_len, d.n * 2, nullptr) != MSW_OK ||
+                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 10, r.d_wlen, d.n * 2, nullptr) != MSW_OK) {
+                            fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
+                            f.failed = true;
+                            break;
+                        }
+                        r.n = d.n;
+                        r.first = d.first_read;
+                        r.fi = fi;
+                        r.live = true;
+                        cur ^= 1;
+                    }
+                    settle(res[cur ^ 1]);
+                    settle(res[cur]);
+                    if (gr) {
+                        uint64_t bi = 0, bo = 0;
+                        msw_gfastq_stats(gr, nullptr, nullptr, nullptr, nullptr, &bi, &bo);
+                        gz_in += bi;
+                        gz_out += bo;
+                    }
+                    msw_gfastq_close(gr);
+                    f.reader_done = true;
+                    finish_file(fi);
+                }
+                for (Res& r : res) {
+                    msw_dev_free(ctx.h, r.d_score);
+                    msw_dev_free(ctx.h, r.d_ei);
+                    msw_dev_free(ctx.h, r.d_ej);
+                    msw_dev_free(ctx.h, r.d_wlen);
+                    msw_host_free(r.h);
+                }
+                msw_genome_destroy(gen);
+                msw_ctx_stats(ctx.h, &gstats[(size_t)gi], 0);
+                gstats[(size_t)gi].alg_bytes = alg_local;
+            });
+        }
+        for (auto& t : workers) t.join();
+        for (size_t fi : todo) finish_file(fi);
+        WgsReport rep;
+        rep.gz_in = gz_in.load();
+        rep.gz_out = gz_out.load();
+        rep.wall_ms = ms_since(t_all);
+        rep.cells = cells.load();
+        rep.readers = 0;
+        rep.host_threads = ngpu;
+        rep.gpu = gstats;
+        rep.gpu_inflate = true;
+        for (size_t i = 0; i < files.size(); ++i)
+            if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
+        return rep;
+    }
 
     // Readers: one thread per lane file in flight (a gzip stream inflates on
     // one core; zlib gives ~0.5-0.75 M reads/s per thread, far below what one
@@ -946,6 +1123,8 @@ int main(int argc, char** argv) {
           << ", \"kernel_ms\": " << kmax << ", \"gpu_busy_fraction\": " << busy
           << ", \"alg_bytes\": " << alg << ", \"hbm_gbps\": " << hbm_gbps
           << ", \"roofline_fraction_hbm\": " << frac_hbm << ", \"roofline_fraction_valu\": " << frac_valu
+          << ", \"gpu_inflate\": " << (rep.gpu_inflate ? "true" : "false")
+          << ", \"inflate_bytes_in\": " << rep.gz_in << ", \"inflate_bytes_out\": " << rep.gz_out
           << ", \"reads_per_second\": " << reads / secs << "}\n";
         write_json(a.json, j.str());
         return all_ok ? 0 : 1;

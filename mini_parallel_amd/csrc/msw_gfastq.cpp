@@ -1,0 +1,611 @@
+// msw_gfastq.cpp -- GPU-side BGZF lane reader (include/msw_fastq.h,
+// msw_gfastq_* and msw_bgzf_inflate).
+//
+// Replaces process_fastq_file_in_chunks (smith_waterman/src/aligner.rs:107-178)
+// for BGZF lane files: the host only reads compressed bytes and indexes the
+// members from their 18-byte headers; everything that touches decompressed
+// bytes runs on the GPU (msw_inflate.hip, msw_parse.hip).
+//
+// One reader = one lane file on one context.  Per span (a few hundred MiB of
+// output, thousands of members):
+//   host    fread compressed bytes into pinned memory, index whole members
+//           (output offsets = running sum of the trailers' ISIZE)
+//   stream  H2D of the bytes + member table; inflate (one wave per member);
+//           CRC-32 check; the previous span's unfinished line copied in front;
+//           parse phase A (line counts) -> host sizes the line arrays ->
+//           phase B (line ends, UTF-8 pass if needed, lengths, carried state)
+//   emit    per batch of max_reads: sequences into a device slab (two slabs
+//           alternate), enqueued on the caller's stream after the parse
+// The reader has its own stream, so the next span inflates while the caller's
+// scoring of the current batch runs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/msw.h"
+#include "../../include/msw_fastq.h"
+#include "msw_gz.h"
+
+namespace msw_detail {
+int set_error(int code, const char* fmt, ...);
+int ctx_device(const msw_ctx* c);
+hipStream_t ctx_compute_stream(const msw_ctx* c);
+}  // namespace msw_detail
+
+using msw_detail::set_error;
+
+namespace {
+
+#define GZ_TRY(expr)                                                                                     \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess)                                                                            \
+            return set_error(MSW_E_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                             __LINE__);                                                                  \
+    } while (0)
+
+constexpr uint64_t kCarry = 64u << 10;     // room in front of a span for the previous span's last line
+constexpr uint64_t kPad = 256;             // device buffers: slack past the end for wide loads
+constexpr uint64_t kReadPiece = 8u << 20;  // compressed bytes per fread
+constexpr uint64_t kDefaultSpan = 256u << 20;
+
+const char* status_text(uint32_t s) {
+    switch (s) {
+        case msw::GZ_E_BTYPE: return "invalid block type";
+        case msw::GZ_E_STORED: return "invalid stored block lengths";
+        case msw::GZ_E_HEADER: return "invalid dynamic block header";
+        case msw::GZ_E_CODES: return "invalid code lengths set";
+        case msw::GZ_E_SYMBOL: return "invalid literal/length or distance code";
+        case msw::GZ_E_DIST: return "invalid distance too far back";
+        case msw::GZ_E_OVERRUN: return "more data than the member's ISIZE";
+        case msw::GZ_E_TRUNC: return "truncated deflate data";
+        case msw::GZ_E_SIZE: return "less data than the member's ISIZE";
+        case msw::GZ_E_CRC: return "incorrect data check";
+        default: return "invalid compressed data";
+    }
+}
+
+// --- CRC-32 combine constants (zlib crc32.c multmodp / x2nmodp) -------------
+uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (uint32_t m = 1u << 31; m; m >>= 1) {
+        if (a & m) p ^= b;
+        b = b & 1 ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+
+msw::GzCrcConsts crc_consts() {
+    msw::GzCrcConsts c;
+    uint32_t p = 1u << 30;  // x^1
+    c.x2n[0] = p;
+    for (int n = 1; n < 32; ++n) c.x2n[n] = p = multmodp(p, p);
+    auto x2nmodp = [&](uint64_t n, unsigned k) {
+        uint32_t q = 1u << 31;
+        while (n) {
+            if (n & 1) q = multmodp(c.x2n[k & 31], q);
+            n >>= 1;
+            ++k;
+        }
+        return q;
+    };
+    for (int k = 0; k < 6; ++k) c.slice[k] = x2nmodp(1024ull << k, 3);
+    return c;
+}
+
+// Size of the BGZF member whose 18-byte header is h, or 0 if h is not one.
+size_t member_size(const uint8_t* h) {
+    if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return 0;
+    const unsigned xlen = h[10] | (h[11] << 8);
+    if (xlen != 6 || h[12] != 'B' || h[13] != 'C' || (h[14] | (h[15] << 8)) != 2) return 0;
+    return (size_t)(h[16] | (h[17] << 8)) + 1;
+}
+
+uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+
+// Whole members of buf[0, n) whose output fits in out_cap more bytes: appended
+// to mem (coff relative to buf, ooff from out_base).  *used = bytes of those
+// members.  Returns MSW_OK, or MSW_E_INVALID for data that is not BGZF.
+int index_members(const uint8_t* buf, size_t n, uint64_t out_base, uint64_t out_cap, std::vector<msw::GzMember>& mem,
+                  size_t* used, uint64_t* out_bytes) {
+    size_t p = 0;
+    uint64_t ob = 0;
+    while (p + 18 <= n) {
+        const size_t sz = member_size(buf + p);
+        if (sz < 26) return set_error(MSW_E_INVALID, "not a BGZF block (mixed gzip members are not supported)");
+        if (p + sz > n) break;
+        const uint32_t isize = le32(buf + p + sz - 4), crc = le32(buf + p + sz - 8);
+        if (isize > 65536) return set_error(MSW_E_INVALID, "BGZF block larger than 64 KiB");
+        if (ob + isize > out_cap) break;
+        msw::GzMember m;
+        m.coff = p + 18;
+        m.ooff = out_base + ob;
+        m.clen = (uint32_t)(sz - 26);
+        m.isize = isize;
+        m.crc = crc;
+        m.pad = 0;
+        mem.push_back(m);
+        p += sz;
+        ob += isize;
+    }
+    *used = p;
+    *out_bytes = ob;
+    return MSW_OK;
+}
+
+template <typename T>
+int grow(T** p, size_t* cap, size_t n) {
+    if (n <= *cap && *p) return MSW_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t want = std::max<size_t>(n, 1) + n / 4;  // headroom against regrowth
+    if (hipMalloc((void**)p, want * sizeof(T) + kPad) != hipSuccess)
+        return set_error(MSW_E_NOMEM, "hipMalloc(%zu) failed (GPU lane reader)", want * sizeof(T) + kPad);
+    *cap = want;
+    return MSW_OK;
+}
+
+// Device side of inflating one group of members (shared by the reader and msw_bgzf_inflate).
+struct Inflater {
+    uint8_t* dc = nullptr;                  // compressed bytes
+    size_t dc_cap = 0;
+    msw::GzMember* d_mem = nullptr;
+    size_t mem_cap = 0;
+    uint32_t* d_status = nullptr;
+    size_t status_cap = 0;
+    uint32_t* d_flag = nullptr;             // [0] any error
+    msw::GzCrcConsts* d_crc = nullptr;
+    uint32_t* h_flag = nullptr;             // pinned
+
+    int init() {
+        GZ_TRY(hipMalloc((void**)&d_flag, 64));
+        GZ_TRY(hipMalloc((void**)&d_crc, sizeof(msw::GzCrcConsts)));
+        const msw::GzCrcConsts c = crc_consts();
+        GZ_TRY(hipMemcpy(d_crc, &c, sizeof(c), hipMemcpyHostToDevice));
+        GZ_TRY(hipHostMalloc((void**)&h_flag, 64, hipHostMallocDefault));
+        return MSW_OK;
+    }
+    void release() {
+        if (dc) (void)hipFree(dc);
+        if (d_mem) (void)hipFree(d_mem);
+        if (d_status) (void)hipFree(d_status);
+        if (d_flag) (void)hipFree(d_flag);
+        if (d_crc) (void)hipFree(d_crc);
+        if (h_flag) (void)hipHostFree(h_flag);
+        dc = nullptr;
+        d_mem = nullptr;
+        d_status = nullptr;
+        d_flag = nullptr;
+        d_crc = nullptr;
+        h_flag = nullptr;
+    }
+    // upload cbytes of compressed data + the member table, inflate into out, check CRCs
+    int run(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, uint8_t* out,
+            hipStream_t s) {
+        int rc;
+        if ((rc = grow(&dc, &dc_cap, cbytes + 64))) return rc;
+        if ((rc = grow(&d_mem, &mem_cap, mem.size()))) return rc;
+        if ((rc = grow(&d_status, &status_cap, mem.size()))) return rc;
+        if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
+        GZ_TRY(hipMemsetAsync(dc + cbytes, 0, 64, s));
+        if (!mem.empty())
+            GZ_TRY(hipMemcpyAsync(d_mem, mem.data(), mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
+        GZ_TRY(hipMemsetAsync(d_flag, 0, 4, s));
+        const uint32_t n = (uint32_t)mem.size();
+        GZ_TRY(msw::launch_gz_inflate(dc, d_mem, n, out, d_status, d_flag, s));
+        GZ_TRY(msw::launch_gz_crc(out, d_mem, n, d_crc, d_status, d_flag, s));
+        GZ_TRY(hipMemcpyAsync(h_flag, d_flag, 4, hipMemcpyDeviceToHost, s));
+        return MSW_OK;
+    }
+    // after the stream synchronised: error message for the first failing member
+    int check(const std::vector<msw::GzMember>& mem, const char* what) {
+        if (!h_flag[0]) return MSW_OK;
+        std::vector<uint32_t> st(mem.size());
+        GZ_TRY(hipMemcpy(st.data(), d_status, st.size() * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < st.size(); ++i)
+            if (st[i]) return set_error(MSW_E_INVALID, "Error reading %s: %s (BGZF member %zu of the span)", what,
+                                        status_text(st[i]), i);
+        return set_error(MSW_E_INVALID, "Error reading %s: invalid compressed data", what);
+    }
+};
+
+}  // namespace
+
+struct msw_gfastq {
+    msw_ctx* ctx = nullptr;
+    int device = 0;
+    hipStream_t rs = nullptr;          // the reader's own stream (inflate + parse)
+    hipEvent_t parsed = nullptr;       // phase B of the current span done
+    hipEvent_t emitted = nullptr;      // the last emit (on the caller's stream)
+    bool emitted_valid = false;
+    FILE* f = nullptr;
+    std::string path;
+    uint64_t fsize = 0, fread_off = 0;
+    uint32_t stride = 0;
+    uint64_t max_reads = 0;
+    bool want_pos = false;
+    uint64_t span = kDefaultSpan;
+
+    // compressed bytes read but not yet inflated: hc[0, hc_len)
+    uint8_t* hc = nullptr;
+    size_t hc_cap = 0, hc_len = 0;
+    Inflater inf;
+    std::vector<msw::GzMember> mem;
+
+    // span buffers: [kCarry | span + kPad]; cur = the parsed one
+    uint8_t* dout[2] = {nullptr, nullptr};
+    int cur = -1;
+    uint64_t cur_off = 0, cur_len = 0, tail_start = 0;  // parse window [cur_off, cur_off + cur_len) of dout[cur]
+    bool started = false, at_eof = false;
+
+    // parse arrays
+    msw::ParseBufs pb{};
+    size_t tile_cap = 0, tile_hi_cap = 0, line_cap = 0, vidx_cap = 0, v_cap = 0, blk_cap = 0;
+    msw::ParseState* d_state = nullptr;
+    msw::ParseOut* d_out = nullptr;
+    msw::ParseOut* h_out = nullptr;  // pinned
+    msw::EmitSpan sp{};
+
+    // batch slabs
+    uint8_t* s_reads[2] = {nullptr, nullptr};
+    uint16_t* s_rlen[2] = {nullptr, nullptr};
+    int64_t* s_pos[2] = {nullptr, nullptr};
+    int slot = 0;
+
+    uint64_t span_reads = 0, span_done = 0, next_first = 0;
+    uint32_t span_min = 0, span_max = 0;
+    int failed = 0;  // sticky error code
+
+    // stats
+    uint64_t lines = 0, reads = 0, errors = 0, bases = 0, bytes_in = 0, bytes_out = 0;
+};
+
+namespace {
+
+void release(msw_gfastq* g) {
+    if (g->f) fclose(g->f);
+    (void)hipSetDevice(g->device);
+    if (g->rs) (void)hipStreamSynchronize(g->rs);
+    for (int i = 0; i < 2; ++i) {
+        if (g->dout[i]) (void)hipFree(g->dout[i]);
+        if (g->s_reads[i]) (void)hipFree(g->s_reads[i]);
+        if (g->s_rlen[i]) (void)hipFree(g->s_rlen[i]);
+        if (g->s_pos[i]) (void)hipFree(g->s_pos[i]);
+    }
+    if (g->pb.tile_nl) (void)hipFree(g->pb.tile_nl);
+    if (g->pb.tile_hi) (void)hipFree(g->pb.tile_hi);
+    if (g->pb.line_end) (void)hipFree(g->pb.line_end);
+    if (g->pb.vidx) (void)hipFree(g->pb.vidx);
+    if (g->pb.vline) (void)hipFree(g->pb.vline);
+    if (g->pb.blk) (void)hipFree(g->pb.blk);
+    if (g->d_state) (void)hipFree(g->d_state);
+    if (g->d_out) (void)hipFree(g->d_out);
+    if (g->h_out) (void)hipHostFree(g->h_out);
+    if (g->hc) (void)hipHostFree(g->hc);
+    g->inf.release();
+    if (g->parsed) (void)hipEventDestroy(g->parsed);
+    if (g->emitted) (void)hipEventDestroy(g->emitted);
+    if (g->rs) (void)hipStreamDestroy(g->rs);
+    delete g;
+}
+
+// Top up hc with compressed bytes from the file (up to cap).
+int fill_compressed(msw_gfastq* g, size_t want) {
+    while (g->hc_len < want && g->fread_off < g->fsize) {
+        const size_t n = (size_t)std::min<uint64_t>(std::min<size_t>(kReadPiece, g->hc_cap - g->hc_len),
+                                                    g->fsize - g->fread_off);
+        if (n == 0) break;
+        const size_t got = fread(g->hc + g->hc_len, 1, n, g->f);
+        if (got != n) return set_error(MSW_E_INVALID, "Error reading %s: short read", g->path.c_str());
+        g->hc_len += got;
+        g->fread_off += got;
+    }
+    return MSW_OK;
+}
+
+// Inflate and parse the next span into dout[next]; sets span_reads (0 is
+// possible: a span without a complete sequence line).  Returns MSW_OK with
+// at_eof set when the file has no more data.
+int next_span(msw_gfastq* g) {
+    int rc;
+    const int nx = g->cur < 0 ? 0 : 1 - g->cur;
+    // 1. whole members whose output fits the span (compressed <= span bytes + 1 MiB)
+    g->mem.clear();
+    size_t used = 0;
+    uint64_t obytes = 0;
+    for (;;) {
+        if ((rc = index_members(g->hc, g->hc_len, kCarry, g->span, g->mem, &used, &obytes))) return rc;
+        const bool full = obytes + 65536 > g->span || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
+        if (full) break;
+        g->mem.clear();
+        if ((rc = fill_compressed(g, g->hc_len + kReadPiece))) return rc;
+    }
+    const bool last = g->fread_off >= g->fsize && used == g->hc_len;
+    if (g->mem.empty() && !last) {
+        if (g->hc_len - used >= 18 && member_size(g->hc + used) > g->hc_cap)
+            return set_error(MSW_E_INVALID, "Error reading %s: BGZF member larger than the staging buffer",
+                             g->path.c_str());
+    }
+    if (g->fread_off >= g->fsize && used < g->hc_len && g->mem.empty())
+        return set_error(MSW_E_INVALID, "Error reading %s: unexpected end of file", g->path.c_str());
+
+    hipStream_t s = g->rs;
+    // the buffer we write and the parse arrays are read by the previous span's emits
+    if (g->emitted_valid) GZ_TRY(hipStreamWaitEvent(s, g->emitted, 0));
+    // 2. inflate + CRC into dout[nx] at kCarry
+    if ((rc = g->inf.run(g->hc, used, g->mem, g->dout[nx], s))) return rc;
+    // 3. the previous span's unfinished line goes right in front
+    const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
+    if (carry > kCarry)
+        return set_error(MSW_E_RANGE, "Error reading %s: a line longer than %llu bytes", g->path.c_str(),
+                         (unsigned long long)kCarry);
+    if (carry)
+        GZ_TRY(hipMemcpyAsync(g->dout[nx] + kCarry - carry, g->dout[g->cur] + g->cur_off + g->tail_start, carry,
+                              hipMemcpyDeviceToDevice, s));
+    // 4. parse phase A over [kCarry - carry, kCarry + obytes), from a 16-byte aligned base
+    msw::ParseBufs& b = g->pb;
+    const uint64_t base = (kCarry - carry) & ~(uint64_t)15;
+    b.buf = g->dout[nx] + base;
+    b.begin = (uint32_t)(kCarry - carry - base);
+    b.len = kCarry + obytes - base;
+    b.eof = last ? 1u : 0u;
+    b.want_pos = g->want_pos ? 1u : 0u;
+    b.ntiles = (uint32_t)((b.len + msw::kParseTile - 1) / msw::kParseTile);
+    if ((rc = grow(&b.tile_nl, &g->tile_cap, (size_t)b.ntiles + 1))) return rc;
+    if ((rc = grow(&b.tile_hi, &g->tile_hi_cap, (size_t)b.ntiles + 1))) return rc;
+    b.line_cap = ~0ull;
+    b.state = g->d_state;
+    b.out = g->d_out;
+    b.stride = g->stride;
+    GZ_TRY(msw::launch_parse_a(b, s));
+    GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
+    GZ_TRY(hipStreamSynchronize(s));
+    if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
+    const uint64_t nlines = g->h_out->lines;
+    const bool any_high = g->h_out->any_high != 0;
+    // 5. size the line arrays, phase B
+    if ((rc = grow(&b.line_end, &g->line_cap, (size_t)nlines + 1))) return rc;
+    b.line_cap = g->line_cap;
+    if (any_high) {
+        if ((rc = grow(&b.vidx, &g->vidx_cap, (size_t)nlines + 1))) return rc;
+        if ((rc = grow(&b.vline, &g->v_cap, (size_t)nlines + 1))) return rc;
+        if ((rc = grow(&b.blk, &g->blk_cap, (size_t)(nlines / 1024 + 2)))) return rc;
+    }
+    GZ_TRY(msw::launch_parse_b(b, nlines, any_high, s));
+    GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
+    GZ_TRY(hipEventRecord(g->parsed, s));
+    GZ_TRY(hipStreamSynchronize(s));
+    const msw::ParseOut& o = *g->h_out;
+    if (o.err_over)
+        return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
+                         (unsigned long long)o.err_line);
+    if (o.too_long)
+        return set_error(MSW_E_RANGE, "sequence longer than the slab stride %u at line %llu", g->stride,
+                         (unsigned long long)o.too_long_line);
+    // consumed compressed bytes leave the staging buffer
+    if (used) {
+        memmove(g->hc, g->hc + used, g->hc_len - used);
+        g->hc_len -= used;
+    }
+    g->bytes_in += used;
+    g->bytes_out += obytes;
+    g->cur = nx;
+    g->cur_off = base;
+    g->cur_len = b.len;
+    g->tail_start = o.tail_start;
+    g->started = true;
+    g->at_eof = last;
+    g->span_reads = o.reads;
+    g->span_done = 0;
+    g->span_min = o.min_len;
+    g->span_max = o.max_len;
+    g->sp.v0 = o.v0;
+    g->sp.pending_in = o.pending_in;
+    g->sp.any_high = o.any_high;
+    g->lines += o.valid;
+    g->errors += o.lines - o.valid;
+    g->reads += o.reads;
+    g->bases += o.bases;
+    return MSW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int msw_is_bgzf(const char* path) {
+    FILE* f = path ? fopen(path, "rb") : nullptr;
+    if (!f) return 0;
+    uint8_t h[18];
+    const bool yes = fread(h, 1, 18, f) == 18 && member_size(h) >= 26;
+    fclose(f);
+    return yes ? 1 : 0;
+}
+
+int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64_t max_reads, int want_pos,
+                    uint64_t span_bytes, msw_gfastq** out) {
+    if (!ctx || !path || !out) return set_error(MSW_E_INVALID, "ctx/path/out is NULL");
+    *out = nullptr;
+    if (read_stride == 0 || read_stride % 16 || read_stride > 256)
+        return set_error(MSW_E_INVALID, "read_stride %u must be a multiple of 16 in [16, 256]", read_stride);
+    if (max_reads == 0) return set_error(MSW_E_INVALID, "max_reads is 0");
+    msw_gfastq* g = new msw_gfastq();
+    g->ctx = ctx;
+    g->device = msw_detail::ctx_device(ctx);
+    g->path = path;
+    g->stride = read_stride;
+    g->max_reads = max_reads;
+    g->want_pos = want_pos != 0;
+    if (span_bytes == 0) {
+        const char* e = getenv("MSW_GFASTQ_SPAN_MB");
+        span_bytes = e && atoll(e) > 0 ? (uint64_t)atoll(e) << 20 : kDefaultSpan;
+    }
+    g->span = std::max<uint64_t>(span_bytes, 1u << 20);
+    if (g->span > (2ull << 30)) g->span = 2ull << 30;  // 32-bit line offsets
+    auto bail = [&](int rc) {
+        release(g);
+        return rc;
+    };
+    g->f = fopen(path, "rb");
+    if (!g->f) return bail(set_error(MSW_E_INVALID, "Failed to open file %s", path));
+    fseeko(g->f, 0, SEEK_END);
+    g->fsize = (uint64_t)ftello(g->f);
+    fseeko(g->f, 0, SEEK_SET);
+    setvbuf(g->f, nullptr, _IONBF, 0);
+    if (g->fsize >= 18) {
+        uint8_t h[18];
+        if (fread(h, 1, 18, g->f) != 18 || member_size(h) < 26)
+            return bail(set_error(MSW_E_INVALID, "%s is not a BGZF file", path));
+        fseeko(g->f, 0, SEEK_SET);
+    } else if (g->fsize > 0) {
+        return bail(set_error(MSW_E_INVALID, "%s is not a BGZF file", path));
+    }
+    if (hipSetDevice(g->device) != hipSuccess) return bail(set_error(MSW_E_DEVICE, "hipSetDevice failed"));
+    int rc;
+    if ((rc = g->inf.init())) return bail(rc);
+    if (hipStreamCreateWithFlags(&g->rs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&g->parsed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->emitted, hipEventDisableTiming) != hipSuccess)
+        return bail(set_error(MSW_E_DEVICE, "stream/event creation failed"));
+    // compressed staging: a span of output is at most ~span compressed bytes (+ headers)
+    g->hc_cap = (size_t)(g->span + g->span / 8 + (4u << 20));
+    if (hipHostMalloc((void**)&g->hc, g->hc_cap, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&g->h_out, sizeof(msw::ParseOut), hipHostMallocDefault) != hipSuccess)
+        return bail(set_error(MSW_E_NOMEM, "hipHostMalloc failed (GPU lane reader staging)"));
+    const size_t ob = (size_t)(kCarry + g->span + kPad);
+    for (int i = 0; i < 2; ++i) {
+        if (hipMalloc((void**)&g->dout[i], ob) != hipSuccess ||
+            hipMalloc((void**)&g->s_reads[i], (size_t)max_reads * read_stride + kPad) != hipSuccess ||
+            hipMalloc((void**)&g->s_rlen[i], (size_t)max_reads * 2 + kPad) != hipSuccess ||
+            (g->want_pos && hipMalloc((void**)&g->s_pos[i], (size_t)max_reads * 8 + kPad) != hipSuccess))
+            return bail(set_error(MSW_E_NOMEM, "hipMalloc failed (GPU lane reader buffers, span %llu MiB)",
+                                  (unsigned long long)(g->span >> 20)));
+    }
+    if (hipMalloc((void**)&g->d_state, sizeof(msw::ParseState)) != hipSuccess ||
+        hipMalloc((void**)&g->d_out, sizeof(msw::ParseOut)) != hipSuccess)
+        return bail(set_error(MSW_E_NOMEM, "hipMalloc failed (GPU lane reader state)"));
+    msw::ParseState st0{0, 0, -1, 0};
+    if (hipMemcpy(g->d_state, &st0, sizeof(st0), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(set_error(MSW_E_DEVICE, "state upload failed"));
+    *out = g;
+    return MSW_OK;
+}
+
+int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {
+    if (!g || !out) return set_error(MSW_E_INVALID, "reader/out is NULL");
+    memset(out, 0, sizeof(*out));
+    out->read_stride = g->stride;
+    if (g->failed) return set_error(g->failed, "Error reading %s: the reader failed earlier", g->path.c_str());
+    if (hipSetDevice(g->device) != hipSuccess) return set_error(MSW_E_DEVICE, "hipSetDevice failed");
+    hipStream_t cs = stream ? (hipStream_t)stream : msw_detail::ctx_compute_stream(g->ctx);
+    while (g->span_done == g->span_reads) {
+        if (g->started && g->at_eof) {
+            out->first_read = g->next_first;
+            return MSW_OK;  // n = 0: end of file
+        }
+        const int rc = next_span(g);
+        if (rc) {
+            g->failed = rc;
+            return rc;
+        }
+    }
+    const uint64_t n = std::min<uint64_t>(g->max_reads, g->span_reads - g->span_done);
+    const int k = g->slot;
+    g->slot ^= 1;
+    GZ_TRY(hipStreamWaitEvent(cs, g->parsed, 0));
+    GZ_TRY(msw::launch_emit_reads(g->pb, g->sp, g->span_done, n, g->s_reads[k], g->s_rlen[k],
+                                  g->want_pos ? g->s_pos[k] : nullptr, cs));
+    GZ_TRY(hipEventRecord(g->emitted, cs));
+    g->emitted_valid = true;
+    out->reads = g->s_reads[k];
+    out->read_len = g->s_rlen[k];
+    out->pos = g->want_pos ? g->s_pos[k] : nullptr;
+    out->n = n;
+    out->first_read = g->next_first;
+    out->min_len = g->span_min;
+    out->max_len = g->span_max;
+    g->span_done += n;
+    g->next_first += n;
+    return MSW_OK;
+}
+
+void msw_gfastq_stats(const msw_gfastq* g, uint64_t* lines, uint64_t* reads, uint64_t* errors, uint64_t* bases,
+                      uint64_t* bytes_in, uint64_t* bytes_out) {
+    if (!g) return;
+    if (lines) *lines = g->lines;
+    if (reads) *reads = g->reads;
+    if (errors) *errors = g->errors;
+    if (bases) *bases = g->bases;
+    if (bytes_in) *bytes_in = g->bytes_in;
+    if (bytes_out) *bytes_out = g->bytes_out;
+}
+
+void msw_gfastq_close(msw_gfastq* g) {
+    if (g) release(g);
+}
+
+int msw_bgzf_inflate(msw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t* out, uint64_t cap,
+                     uint64_t* out_len) {
+    if (!ctx || (!data && len) || !out_len) return set_error(MSW_E_INVALID, "ctx/data/out_len is NULL");
+    *out_len = 0;
+    GZ_TRY(hipSetDevice(msw_detail::ctx_device(ctx)));
+    hipStream_t s = msw_detail::ctx_compute_stream(ctx);
+    Inflater inf;
+    int rc = inf.init();
+    uint8_t* dout = nullptr;
+    uint8_t* hstage = nullptr;
+    constexpr uint64_t kGroup = 256u << 20;  // output bytes per launch
+    uint64_t p = 0, total = 0;
+    std::vector<msw::GzMember> mem;
+    while (!rc && p < len) {
+        mem.clear();
+        size_t used = 0;
+        uint64_t ob = 0;
+        rc = index_members(data + p, (size_t)(len - p), 0, kGroup, mem, &used, &ob);
+        if (rc) break;
+        if (mem.empty()) {
+            rc = set_error(MSW_E_INVALID, "unexpected end of file");
+            break;
+        }
+        if (total + ob > cap) {
+            rc = set_error(MSW_E_RANGE, "output buffer of %llu bytes is too small", (unsigned long long)cap);
+            break;
+        }
+        if (!dout && hipMalloc((void**)&dout, kGroup + kPad) != hipSuccess) {
+            rc = set_error(MSW_E_NOMEM, "hipMalloc failed");
+            break;
+        }
+        if (!hstage && hipHostMalloc((void**)&hstage, kGroup + kGroup / 8 + (4u << 20)) != hipSuccess) {
+            rc = set_error(MSW_E_NOMEM, "hipHostMalloc failed");
+            break;
+        }
+        memcpy(hstage, data + p, used);
+        if ((rc = inf.run(hstage, used, mem, dout, s))) break;
+        if (hipStreamSynchronize(s) != hipSuccess) {
+            rc = set_error(MSW_E_DEVICE, "inflate launch failed");
+            break;
+        }
+        if ((rc = inf.check(mem, "BGZF data"))) break;
+        if (ob && hipMemcpy(out + total, dout, ob, hipMemcpyDeviceToHost) != hipSuccess) {
+            rc = set_error(MSW_E_DEVICE, "D2H failed");
+            break;
+        }
+        total += ob;
+        p += used;
+    }
+    if (dout) (void)hipFree(dout);
+    if (hstage) (void)hipHostFree(hstage);
+    inf.release();
+    if (!rc) *out_len = total;
+    return rc;
+}
+
+}  // extern "C"

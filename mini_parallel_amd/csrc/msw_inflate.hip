@@ -1,0 +1,500 @@
+// msw_inflate.hip -- BGZF member inflate (RFC 1951 DEFLATE) and CRC-32 check
+// on gfx950, one wave per member.
+//
+// Why on the GPU: the --full-wgs lane files are gzip'ed FASTQ.  The reference
+// pipes each through `zcat` and splits lines into Strings on one core per file
+// (smith_waterman/src/aligner.rs:107-178); even libdeflate on the host tops
+// out near 1.6 M reads/s per CPU, two orders of magnitude below
+// what one MI355X scores.  BGZF members are independent deflate streams of
+// <= 64 KiB output whose sizes are in their headers, so a span of thousands of
+// members inflates with thousands of waves at once and only compressed bytes
+// cross PCIe.
+//
+// Mapping.  Huffman decoding is a serial chain per member, so a wave owns a
+// member and runs the chain on wave-uniform values (SGPRs; the compiler sees
+// them as uniform); the 64 lanes are used where the format is parallel:
+//  * canonical decode without lookup tables: lane L (1..15) holds the
+//    left-justified end of the codes of length <= L; one compare + ballot
+//    finds the code length of the next 15 stream bits, v_readlane fetches the
+//    length's base, and ONE LDS read maps the code to its symbol (the
+//    sorted-symbol array, <= 288 u16), so a dynamic block's tables cost
+//    ~650 B of LDS and a few hundred instructions to build;
+//  * the last 4 KiB of output live in an LDS ring: literals are single-lane
+//    byte writes, a match copies up to 64 bytes per instruction from the ring
+//    (overlapping copies index the source modulo the distance), and every
+//    completed 256-byte chunk is flushed to HBM with one coalesced store per
+//    lane; matches reaching further back than the ring read the flushed
+//    output from L2 (agent-scope loads after the flush stores have drained);
+//  * the CRC-32 check is a second kernel: each lane CRCs a 1 KiB slice of the
+//    member's output and the 64 slice CRCs are combined in a 6-level tree
+//    with GF(2) shift constants (zlib's crc32_combine).
+// Errors follow zlib's inflate (inftrees.c rules for code sets): any error
+// marks the member and stops its wave; no byte is ever written outside the
+// member's ISIZE bytes of output.
+#include "msw_gz.h"
+
+namespace msw {
+namespace {
+
+constexpr uint32_t kRing = 4096;  // LDS window of the most recent output bytes
+constexpr uint32_t kRingMask = kRing - 1;
+constexpr uint32_t kChunk = 256;  // flush unit: 64 lanes x 4 bytes
+
+// order of the code-length code lengths in a dynamic block header
+__constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct __align__(16) InflateLds {
+    uint32_t ring32[kRing / 4];
+    uint16_t sym_ll[288];  // lit/len symbols sorted by (code length, symbol)
+    uint16_t sym_d[32];    // distance symbols
+    uint16_t sym_c[20];    // code-length alphabet
+    uint8_t lens[320];     // code lengths of the block being built (<= 286 + 30)
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
+
+// zlib inftrees.c rules: kind 0 = code-length code (must be complete),
+// 1 = lit/len, 2 = distance (incomplete only as a single 1-bit code).
+// Builds the sorted symbol array and each lane's (lj_end, base) pair:
+// lane L in 1..15 gets lim = (first[L] + count[L]) << (15 - L) and
+// bas = offs[L] - first[L]; other lanes lim = 0.  Returns false on an
+// over-subscribed or (disallowed) incomplete set.
+__device__ bool build_code(const uint8_t* lens, uint32_t n, uint16_t* syms, uint32_t& lim, int32_t& bas,
+                           int kind) {
+    const uint32_t lane = lane_id();
+    uint32_t cnt = 0;
+    for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        const uint32_t L = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (uint32_t l = 1; l <= 15; ++l) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(L == l));
+            if (lane == l) cnt += c;
+        }
+    }
+    uint32_t code = 0, off = 0, maxlen = 0, slot = 0;
+    int32_t left = 1;
+    lim = 0;
+    bas = 0;
+#pragma unroll
+    for (uint32_t L = 1; L <= 15; ++L) {
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)L);
+        if (lane == L) {
+            lim = (code + c) << (15 - L);
+            bas = (int32_t)off - (int32_t)code;
+            slot = off;
+        }
+        left = (left << 1) - (int32_t)c;
+        if (left < 0) return false;  // over-subscribed
+        if (c) maxlen = L;
+        off += c;
+        code = (code + c) << 1;
+    }
+    if (maxlen == 0) {  // no codes: every decode fails (a distance code may be unused)
+        lim = 0;
+        return kind != 1;
+    }
+    if (left > 0 && (kind == 0 || maxlen != 1)) return false;  // incomplete set
+    // symbols sorted by (length, symbol): rank within a length by ballot
+    for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        const uint32_t L = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (uint32_t l = 1; l <= 15; ++l) {
+            const uint64_t m = __ballot(L == l);
+            if (m) {
+                const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)slot, (int)l);
+                if (L == l) {
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    syms[base + below] = (uint16_t)s;
+                }
+                if (lane == l) slot += (uint32_t)__popcll(m);
+            }
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+// The bit reader: stream bits LSB-first from a 64-bit buffer refilled with
+// aligned dwords (one prefetched ahead).  All fields are wave-uniform.
+struct Bits {
+    const uint32_t* src;  // the span's compressed buffer as dwords
+    uint64_t bb;
+    uint32_t bcnt;        // valid bits in bb
+    uint32_t wi;          // dword index of nxt
+    uint32_t nxt;         // src[wi], loaded ahead
+    uint32_t wmax;        // refills past this dword index mean truncated data
+
+    __device__ __forceinline__ void prime(uint64_t byte_pos) {
+        const uint32_t w = (uint32_t)(byte_pos >> 2), sh = 8u * (uint32_t)(byte_pos & 3);
+        bb = (uint64_t)(src[w] >> sh);
+        bcnt = 32u - sh;
+        wi = w + 1;
+        nxt = src[wi];
+    }
+    // true if the refill stayed within the member (+ slack)
+    __device__ __forceinline__ bool refill() {
+        if (bcnt < 32) {
+            bb |= (uint64_t)nxt << bcnt;
+            bcnt += 32;
+            ++wi;
+            if (wi > wmax) return false;
+            nxt = src[wi];
+        }
+        return true;
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
+    __device__ __forceinline__ void drop(uint32_t n) {
+        bb >>= n;
+        bcnt -= n;
+    }
+    __device__ __forceinline__ uint32_t take(uint32_t n) {
+        const uint32_t v = peek(n);
+        drop(n);
+        return v;
+    }
+    // stream bits consumed since byte 0 of the buffer
+    __device__ __forceinline__ uint64_t bit_pos() const { return (uint64_t)wi * 32u - bcnt; }
+};
+
+// One Huffman symbol (canonical decode, see the file comment); -1 if the
+// next bits are no code of this set.  Needs bcnt >= 15.
+__device__ __forceinline__ int decode_sym(Bits& br, uint32_t lim, int32_t bas, const uint16_t* syms) {
+    const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;  // next 15 bits, first as MSB
+    const uint64_t m = __ballot(r < lim);
+    if (m == 0) return -1;
+    const uint32_t L = (uint32_t)__builtin_ctzll(m);
+    const int32_t base = __builtin_amdgcn_readlane(bas, (int)L);
+    const uint32_t idx = (uint32_t)(base + (int32_t)(r >> (15 - L)));
+    br.drop(L);
+    return (int)__builtin_amdgcn_readfirstlane((uint32_t)syms[idx]);
+}
+
+__device__ __forceinline__ uint32_t coherent_load(const uint8_t* p) {
+    return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) void gz_inflate_kernel(const uint8_t* __restrict__ cdata,
+                                                        const GzMember* __restrict__ members, uint32_t n,
+                                                        uint8_t* __restrict__ out, uint32_t* __restrict__ status,
+                                                        uint32_t* __restrict__ any_error) {
+    __shared__ InflateLds S;
+    const uint32_t m = blockIdx.x;
+    if (m >= n) return;
+    const uint32_t lane = lane_id();
+    uint8_t* ring = (uint8_t*)S.ring32;
+    const GzMember mem = members[m];
+    uint8_t* dst = out + mem.ooff;
+    const uint32_t isize = mem.isize;
+    const bool dst_al4 = (mem.ooff & 3) == 0;
+
+    Bits br;
+    br.src = (const uint32_t*)cdata;
+    br.wmax = (uint32_t)((mem.coff + mem.clen) >> 2) + 2u;
+    br.prime(mem.coff);
+
+    uint32_t opos = 0, flushed = 0, err = GZ_OK;
+    uint32_t lim_ll = 0, lim_d = 0, lim_c = 0;
+    int32_t bas_ll = 0, bas_d = 0, bas_c = 0;
+    int tables = -1;  // 1 = fixed tables loaded, 2 = dynamic
+
+    // flush [from, from + 256) of the output (ring-resident) to HBM
+    auto flush_chunk = [&](uint32_t from) __attribute__((always_inline)) {
+        const uint32_t v = S.ring32[((from + 4u * lane) & kRingMask) >> 2];
+        uint8_t* d = dst + from + 4u * lane;
+        if (dst_al4) {
+            *(uint32_t*)d = v;
+        } else {
+            d[0] = (uint8_t)v;
+            d[1] = (uint8_t)(v >> 8);
+            d[2] = (uint8_t)(v >> 16);
+            d[3] = (uint8_t)(v >> 24);
+        }
+    };
+
+    bool last = false;
+    while (!last && err == GZ_OK) {
+        if (!br.refill()) { err = GZ_E_TRUNC; break; }
+        const uint32_t hdr = br.take(3);
+        last = (hdr & 1u) != 0;
+        const uint32_t btype = hdr >> 1;
+        if (btype == 0) {
+            // stored block: byte-align, LEN, NLEN, LEN raw bytes
+            br.drop(br.bcnt & 7u);
+            if (!br.refill()) { err = GZ_E_TRUNC; break; }
+            const uint32_t len = br.take(16), nlen = br.take(16);
+            if (len != (~nlen & 0xFFFFu)) { err = GZ_E_STORED; break; }
+            if (opos + len > isize) { err = GZ_E_OVERRUN; break; }
+            uint32_t k = 0;
+            while (k < len && br.bcnt >= 8) {  // bytes already in the bit buffer
+                const uint32_t v = br.take(8);
+                if (lane == 0) ring[opos & kRingMask] = (uint8_t)v;
+                ++opos;
+                ++k;
+                if ((opos & (kChunk - 1)) == 0) { flush_chunk(opos - kChunk); flushed = opos; }
+            }
+            if (k < len) {
+                // the buffer is empty: the stream continues at byte 4 * wi
+                uint64_t p = (uint64_t)br.wi * 4u;
+                const uint32_t rest = len - k;
+                if (p + rest > mem.coff + mem.clen) { err = GZ_E_TRUNC; break; }
+                for (uint32_t j0 = 0; j0 < rest; j0 += kChunk) {
+                    const uint32_t j = j0 + 4u * lane;
+                    if (j < rest) {
+                        const uint64_t q = p + j;
+                        const uint32_t lo = br.src[q >> 2], hi = br.src[(q >> 2) + 1];
+                        const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(q & 3));
+                        const uint32_t nb = min(4u, rest - j);
+                        // opos already counts the earlier rounds (j0 bytes)
+                        for (uint32_t b = 0; b < nb; ++b)
+                            ring[(opos + 4u * lane + b) & kRingMask] = (uint8_t)(v >> (8 * b));
+                    }
+                    const uint32_t adv = min(kChunk, rest - j0);
+                    opos += adv;
+                    while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
+                }
+                br.prime(p + rest);
+            }
+            continue;
+        }
+        if (btype == 3) { err = GZ_E_BTYPE; break; }
+        if (btype == 1) {
+            if (tables != 1) {
+                for (uint32_t s = lane; s < 288; s += 64)
+                    S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                __syncthreads();
+                build_code(S.lens, 288, S.sym_ll, lim_ll, bas_ll, 1);
+                for (uint32_t s = lane; s < 32; s += 64) S.lens[s] = 5;
+                __syncthreads();
+                build_code(S.lens, 32, S.sym_d, lim_d, bas_d, 2);
+                tables = 1;
+            }
+        } else {
+            // dynamic block header
+            if (!br.refill()) { err = GZ_E_TRUNC; break; }
+            const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
+            if (nlen > 286 || ndist > 30) { err = GZ_E_HEADER; break; }
+            if (lane < 19) S.lens[lane] = 0;
+            __syncthreads();
+            // code-length code lengths, 3 bits each, in kClOrder (RFC 1951 3.2.7)
+            for (uint32_t i = 0; i < ncode; ++i) {
+                if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                const uint32_t v = br.take(3);
+                if (lane == 0) S.lens[kClOrder[i]] = (uint8_t)v;
+            }
+            if (err) break;
+            __syncthreads();
+            if (!build_code(S.lens, 19, S.sym_c, lim_c, bas_c, 0)) { err = GZ_E_CODES; break; }
+            // lit/len + distance code lengths (one sequence; repeats may cross)
+            const uint32_t total = nlen + ndist;
+            uint32_t idx = 0;
+            while (idx < total) {
+                if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                const int sym = decode_sym(br, lim_c, bas_c, S.sym_c);
+                if (sym < 0) { err = GZ_E_CODES; break; }
+                if (sym < 16) {
+                    if (lane == 0) S.lens[idx] = (uint8_t)sym;
+                    ++idx;
+                    continue;
+                }
+                uint32_t rep, val = 0;
+                if (sym == 16) {
+                    if (idx == 0) { err = GZ_E_HEADER; break; }
+                    val = __builtin_amdgcn_readfirstlane((uint32_t)S.lens[idx - 1]);
+                    rep = 3 + br.take(2);
+                } else if (sym == 17) {
+                    rep = 3 + br.take(3);
+                } else {
+                    rep = 11 + br.take(7);
+                }
+                if (idx + rep > total) { err = GZ_E_HEADER; break; }
+                for (uint32_t k = lane; k < rep; k += 64) S.lens[idx + k] = (uint8_t)val;
+                idx += rep;
+            }
+            if (err) break;
+            __syncthreads();
+            if (S.lens[256] == 0) { err = GZ_E_CODES; break; }
+            if (!build_code(S.lens, nlen, S.sym_ll, lim_ll, bas_ll, 1)) { err = GZ_E_CODES; break; }
+            if (!build_code(S.lens + nlen, ndist, S.sym_d, lim_d, bas_d, 2)) { err = GZ_E_CODES; break; }
+            tables = 2;
+        }
+        // Huffman-coded data until end-of-block
+        for (;;) {
+            if (!br.refill()) { err = GZ_E_TRUNC; break; }
+            const int sym = decode_sym(br, lim_ll, bas_ll, S.sym_ll);
+            if (sym < 0) { err = GZ_E_SYMBOL; break; }
+            if (sym < 256) {
+                if (opos >= isize) { err = GZ_E_OVERRUN; break; }
+                if (lane == 0) ring[opos & kRingMask] = (uint8_t)sym;
+                ++opos;
+                if ((opos & (kChunk - 1)) == 0) { flush_chunk(opos - kChunk); flushed = opos; }
+                continue;
+            }
+            if (sym == 256) break;
+            if (sym > 285) { err = GZ_E_SYMBOL; break; }
+            // length: 257..264 -> 3..10, 265..284 -> base + extra bits, 285 -> 258
+            uint32_t len;
+            if (sym < 265) {
+                len = (uint32_t)sym - 254;
+            } else if (sym < 285) {
+                const uint32_t e = ((uint32_t)sym - 261) >> 2;
+                len = ((4u + (((uint32_t)sym - 265) & 3u)) << e) + 3u + br.take(e);
+            } else {
+                len = 258;
+            }
+            if (!br.refill()) { err = GZ_E_TRUNC; break; }
+            const int ds = decode_sym(br, lim_d, bas_d, S.sym_d);
+            if (ds < 0 || ds > 29) { err = GZ_E_SYMBOL; break; }
+            uint32_t dist;
+            if (ds < 4) {
+                dist = (uint32_t)ds + 1;
+            } else {
+                const uint32_t e = ((uint32_t)ds >> 1) - 1;
+                dist = ((2u + ((uint32_t)ds & 1u)) << e) + 1u + br.take(e);
+            }
+            if (dist > opos) { err = GZ_E_DIST; break; }
+            if (opos + len > isize) { err = GZ_E_OVERRUN; break; }
+            if (dist + len <= kRing) {
+                // ring -> ring; the source is the `dist` bytes before opos,
+                // read modulo dist when the copy overlaps itself
+                const float rd = __builtin_amdgcn_rcpf((float)dist);
+                for (uint32_t j0 = 0; j0 < len; j0 += 64) {
+                    const uint32_t j = j0 + lane;
+                    uint32_t s = j;
+                    if (dist < len) {
+                        int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
+                        if (r < 0) r += (int32_t)dist;
+                        if (r >= (int32_t)dist) r -= (int32_t)dist;
+                        s = (uint32_t)r;
+                    }
+                    uint8_t v = 0;
+                    if (j < len) v = ring[(opos - dist + s) & kRingMask];
+                    if (j < len) ring[(opos + j) & kRingMask] = v;
+                }
+            } else {
+                // further back than the ring: the flushed output in L2 (the
+                // source ends >= 3.5 KiB before opos, i.e. before `flushed`)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
+                for (uint32_t j0 = 0; j0 < len; j0 += kChunk) {
+                    const uint32_t j = j0 + 4u * lane;
+                    if (j < len) {
+                        const uint64_t q = mem.ooff + (uint64_t)(opos - dist + j);
+                        const uint8_t* a = out + (q & ~(uint64_t)3);
+                        const uint32_t lo = coherent_load(a), hi = coherent_load(a + 4);
+                        const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(q & 3));
+                        const uint32_t nb = min(4u, len - j);
+                        for (uint32_t b = 0; b < nb; ++b) ring[(opos + j + b) & kRingMask] = (uint8_t)(v >> (8 * b));
+                    }
+                }
+            }
+            opos += len;
+            while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
+        }
+    }
+    if (err == GZ_OK) {
+        if (opos != isize) err = GZ_E_SIZE;
+        else if ((br.bit_pos() - mem.coff * 8u + 7u) / 8u > mem.clen) err = GZ_E_TRUNC;
+    }
+    if (err == GZ_OK) {
+        // the last partial chunk
+        for (uint32_t k = lane; k < opos - flushed; k += 64) dst[flushed + k] = ring[(flushed + k) & kRingMask];
+    }
+    if (lane == 0) {
+        status[m] = err;
+        if (err) atomicOr(any_error, 1u);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CRC-32 (zlib's polynomial, reflected) of each member's output.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPoly = 0xEDB88320u;
+
+__device__ uint32_t multmodp(uint32_t a, uint32_t b) {  // a * b mod p(x), reflected (x^0 = bit 31)
+    uint32_t p = 0;
+    for (uint32_t m = 1u << 31; m; m >>= 1) {
+        if (a & m) p ^= b;
+        b = b & 1 ? (b >> 1) ^ kPoly : b >> 1;
+    }
+    return p;
+}
+
+__device__ uint32_t x2nmodp(const GzCrcConsts& c, uint64_t n, uint32_t k) {  // x^(n * 2^k) mod p
+    uint32_t p = 1u << 31;
+    while (n) {
+        if (n & 1) p = multmodp(c.x2n[k & 31], p);
+        n >>= 1;
+        ++k;
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(64) void gz_crc_kernel(const uint8_t* __restrict__ out,
+                                                    const GzMember* __restrict__ members, uint32_t n,
+                                                    const GzCrcConsts* __restrict__ consts,
+                                                    uint32_t* __restrict__ status, uint32_t* __restrict__ any_error) {
+    __shared__ uint32_t T[256];
+    const uint32_t m = blockIdx.x;
+    if (m >= n) return;
+    const uint32_t lane = lane_id();
+    for (uint32_t i = lane; i < 256; i += 64) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = c & 1 ? (c >> 1) ^ kPoly : c >> 1;
+        T[i] = c;
+    }
+    __syncthreads();
+    if (status[m] != GZ_OK) return;  // inflate already failed
+    const GzMember mem = members[m];
+    // Virtual 64 KiB of output, zero-padded at the front (a raw CRC -- no
+    // pre/post conditioning -- of leading zeros is 0): lane l owns virtual
+    // bytes [1024 l, 1024 l + 1024), so every tree node has a power-of-two size.
+    const uint32_t pad = 65536u - mem.isize;
+    const uint32_t a = max(1024u * lane, pad) - pad, b = max(1024u * (lane + 1), pad) - pad;
+    const uint8_t* p = out + mem.ooff;
+    uint32_t c = 0;
+    uint32_t i = a;
+    for (; i < b && ((mem.ooff + i) & 3); ++i) c = T[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    for (; i + 4 <= b; i += 4) {
+        c ^= *(const uint32_t*)(p + i);
+        c = T[c & 0xFF] ^ (c >> 8);
+        c = T[c & 0xFF] ^ (c >> 8);
+        c = T[c & 0xFF] ^ (c >> 8);
+        c = T[c & 0xFF] ^ (c >> 8);
+    }
+    for (; i < b; ++i) c = T[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    // tree: raw(A || B) = raw(A) * x^(8|B|) ^ raw(B)
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) {
+        const uint32_t step = 1u << k;
+        const uint32_t right = __shfl_down(c, step);
+        if ((lane & (2 * step - 1)) == 0) c = multmodp(consts->slice[k], c) ^ right;
+    }
+    if (lane == 0) {
+        // standard CRC: pre-condition 0xFFFFFFFF shifted over the data, post-xor
+        const uint32_t crc = c ^ multmodp(x2nmodp(*consts, mem.isize, 3), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        if (crc != mem.crc) {
+            status[m] = GZ_E_CRC;
+            atomicOr(any_error, 1u);
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint32_t n, uint8_t* out,
+                             uint32_t* status, uint32_t* any_error, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gz_inflate_kernel, dim3(n), dim3(64), 0, stream, cdata, members, n, out, status, any_error);
+    return hipGetLastError();
+}
+
+hipError_t launch_gz_crc(const uint8_t* out, const GzMember* members, uint32_t n, const GzCrcConsts* consts,
+                         uint32_t* status, uint32_t* any_error, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gz_crc_kernel, dim3(n), dim3(64), 0, stream, out, members, n, consts, status, any_error);
+    return hipGetLastError();
+}
+
+}  // namespace msw

@@ -134,6 +134,11 @@ hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, 
 constexpr uint32_t kGenomePad = 64;
 hipError_t launch_cut_windows(const uint8_t* genome, uint64_t glen, const int64_t* pos, const uint16_t* want,
                               uint8_t* out, uint16_t* out_len, uint32_t ws, uint64_t n, hipStream_t stream);
+// Same, for device-resident reads: want = window, or 2 x rlen[p] when window
+// is 0, capped at kMaxWinLen (msw_align_reads_device).
+hipError_t launch_cut_windows_for_reads(const uint8_t* genome, uint64_t glen, const int64_t* pos,
+                                        const uint16_t* rlen, uint32_t window, uint8_t* out, uint16_t* out_len,
+                                        uint32_t ws, uint64_t n, hipStream_t stream);
 
 // dst[i] = src[inv[i]] for score (and end_i / end_j when non-null): pair
 // order restored from slot-ordered results (one thread per pair, coalesced

@@ -54,6 +54,7 @@ __global__ __launch_bounds__(256) void sw_compat_kernel(const uint8_t* __restric
 __global__ __launch_bounds__(256) void cut_windows_kernel(const uint8_t* __restrict__ g, uint64_t glen,
                                                           const int64_t* __restrict__ pos,
                                                           const uint16_t* __restrict__ want,
+                                                          const uint16_t* __restrict__ rlen, uint32_t window,
                                                           uint8_t* __restrict__ out, uint16_t* __restrict__ out_len,
                                                           uint32_t chunks, uint64_t ws, uint64_t n) {
     const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -62,7 +63,9 @@ __global__ __launch_bounds__(256) void cut_windows_kernel(const uint8_t* __restr
     const uint32_t c = (uint32_t)(t - p * chunks);
     const uint64_t start = (uint64_t)pos[p];  // negative positions wrap past glen
     const uint64_t room = start < glen ? glen - start : 0;
-    const int len = (int)min(min((uint64_t)want[p], room), ws);
+    // requested length: want[p], or (device-resident reads) --window / 2 x read length
+    const uint64_t wl = want ? want[p] : min(window ? window : 2u * rlen[p], (uint32_t)kMaxWinLen);
+    const int len = (int)min(min(wl, room), ws);
     if (out_len && c == 0) out_len[p] = (uint16_t)len;
     const int rem = len - 16 * (int)c;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -147,8 +150,21 @@ hipError_t launch_cut_windows(const uint8_t* genome, uint64_t glen, const int64_
     const uint32_t chunks = ws / 16;
     const uint64_t blocks = (n * chunks + 255) / 256;
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(cut_windows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, genome, glen, pos, want, out,
-                       out_len, chunks, (uint64_t)ws, n);
+    hipLaunchKernelGGL(cut_windows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, genome, glen, pos, want,
+                       (const uint16_t*)nullptr, 0u, out, out_len, chunks, (uint64_t)ws, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_cut_windows_for_reads(const uint8_t* genome, uint64_t glen, const int64_t* pos,
+                                        const uint16_t* rlen, uint32_t window, uint8_t* out, uint16_t* out_len,
+                                        uint32_t ws, uint64_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (ws == 0 || ws % 16 != 0 || ((uintptr_t)out & 15) != 0) return hipErrorInvalidValue;
+    const uint32_t chunks = ws / 16;
+    const uint64_t blocks = (n * chunks + 255) / 256;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cut_windows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, genome, glen, pos,
+                       (const uint16_t*)nullptr, rlen, window, out, out_len, chunks, (uint64_t)ws, n);
     return hipGetLastError();
 }
 

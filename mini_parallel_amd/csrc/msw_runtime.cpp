@@ -222,6 +222,17 @@ struct msw_ctx {
     int32_t* c_res = nullptr;
     size_t c_cap = 0;
     hipEvent_t c_k0 = nullptr, c_k1 = nullptr;  // timing of the compat launch (msw_ctx_stats)
+    // msw_align_reads_device scratch: the cut windows and their clipped lengths
+    uint8_t* r_wins = nullptr;
+    uint16_t* r_wlen = nullptr;
+    size_t r_wins_cap = 0, r_wlen_cap = 0;
+    // timing events of msw_align_reads_device launches not yet harvested
+    struct DevTiming {
+        hipEvent_t k0, k1;
+        uint64_t pairs;
+    };
+    std::deque<DevTiming> dev_timings;
+    std::vector<hipEvent_t> free_events;
 };
 
 struct msw_genome {
@@ -231,6 +242,12 @@ struct msw_genome {
     uint64_t len = 0;
 };
 
+// Internal accessors for the other units of the library (msw_gfastq.cpp).
+namespace msw_detail {
+int ctx_device(const msw_ctx* c) { return c->device; }
+hipStream_t ctx_compute_stream(const msw_ctx* c) { return c->compute; }
+}  // namespace msw_detail
+
 namespace {
 
 int set_device(msw_ctx* ctx) {
@@ -238,6 +255,33 @@ int set_device(msw_ctx* ctx) {
     if (hipGetDevice(&cur) == hipSuccess && cur == ctx->device) return MSW_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     return MSW_OK;
+}
+
+hipEvent_t take_event(msw_ctx* ctx) {
+    if (!ctx->free_events.empty()) {
+        hipEvent_t e = ctx->free_events.back();
+        ctx->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+
+// Kernel time of finished msw_align_reads_device launches into ctx->stats
+// (wait = true: all of them, after synchronising).
+void harvest_dev_timings(msw_ctx* ctx, bool wait) {
+    while (!ctx->dev_timings.empty()) {
+        msw_ctx::DevTiming& t = ctx->dev_timings.front();
+        if (wait) (void)hipEventSynchronize(t.k1);
+        else if (hipEventQuery(t.k1) != hipSuccess) break;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, t.k0, t.k1) == hipSuccess) ctx->stats.kernel_ms += ms;
+        ctx->stats.launches += 1;
+        ctx->stats.pairs += t.pairs;
+        ctx->free_events.push_back(t.k0);
+        ctx->free_events.push_back(t.k1);
+        ctx->dev_timings.pop_front();
+    }
 }
 
 template <typename T>
@@ -937,6 +981,13 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     (void)hipFree(ctx->c_s1);
     (void)hipFree(ctx->c_s2);
     (void)hipFree(ctx->c_res);
+    (void)hipFree(ctx->r_wins);
+    (void)hipFree(ctx->r_wlen);
+    for (auto& t : ctx->dev_timings) {
+        (void)hipEventDestroy(t.k0);
+        (void)hipEventDestroy(t.k1);
+    }
+    for (hipEvent_t e : ctx->free_events) (void)hipEventDestroy(e);
     if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
@@ -1301,6 +1352,54 @@ int msw_align_reads_async(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genom
     return MSW_OK;
 }
 
+int msw_align_reads_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_genome* g, const uint8_t* reads,
+                           const uint16_t* read_len, uint32_t read_stride, const int64_t* win_pos, uint64_t n,
+                           uint32_t window, uint32_t max_read_len, msw_out_t* out, uint16_t* win_len_out,
+                           void* stream) {
+    if (!ctx || !g) return fail(MSW_E_INVALID, "ctx/genome is NULL");
+    if (g->ctx != ctx) return fail(MSW_E_INVALID, "genome belongs to another context");
+    if (n == 0) return MSW_OK;
+    if (!reads || !read_len || !win_pos || !out || !out->score) return fail(MSW_E_INVALID, "NULL array");
+    if (window > (uint32_t)msw::kMaxWinLen) return fail(MSW_E_RANGE, "window %u > %d", window, msw::kMaxWinLen);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    const uint32_t max_win = window ? window : std::min<uint32_t>(2u * max_read_len, (uint32_t)msw::kMaxWinLen);
+    const uint32_t ws = std::max<uint32_t>(16u, (max_win + 15u) & ~15u);
+    const size_t wbytes = (size_t)n * ws;
+    if (wbytes > ctx->r_wins_cap) {
+        if ((rc = grow_dev(&ctx->r_wins, wbytes + wbytes / 4))) return rc;
+        ctx->r_wins_cap = wbytes + wbytes / 4;
+    }
+    uint16_t* wlen = win_len_out;
+    if (!wlen) {
+        if (n > ctx->r_wlen_cap) {
+            if ((rc = grow_dev(&ctx->r_wlen, (size_t)n + n / 4))) return rc;
+            ctx->r_wlen_cap = (size_t)n + n / 4;
+        }
+        wlen = ctx->r_wlen;
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    harvest_dev_timings(ctx, false);
+    HIP_TRY(msw::launch_cut_windows_for_reads(g->d_seq, g->len, win_pos, read_len, window, ctx->r_wins, wlen, ws, n,
+                                              st));
+    msw_batch_t b{reads, ctx->r_wins, read_len, wlen, read_stride, ws, n};
+    msw_ctx::DevTiming t{take_event(ctx), take_event(ctx), n};
+    if (!t.k0 || !t.k1) return fail(MSW_E_DEVICE, "hipEventCreate failed");
+    HIP_TRY(hipEventRecord(t.k0, st));
+    if ((rc = msw_align_batch_device(ctx, sc, &b, out, max_read_len, max_win, stream))) return rc;
+    HIP_TRY(hipEventRecord(t.k1, st));
+    ctx->dev_timings.push_back(t);
+    return MSW_OK;
+}
+
+int msw_memcpy_d2h_async(msw_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream ? (hipStream_t)stream : ctx->compute));
+    return MSW_OK;
+}
+
 void* msw_host_alloc(size_t bytes) {
     void* p = nullptr;
     // portable: the --full-wgs readers fill slabs that any GPU's context DMAs
@@ -1348,6 +1447,7 @@ int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes) {
 
 int msw_ctx_stats(msw_ctx* ctx, msw_stats_t* out, int reset) {
     if (!ctx || !out) return fail(MSW_E_INVALID, "ctx/out is NULL");
+    if (set_device(ctx) == MSW_OK) harvest_dev_timings(ctx, true);
     *out = ctx->stats;
     if (reset) ctx->stats = msw_stats_t{};
     return MSW_OK;

@@ -11,7 +11,7 @@ from typing import Callable, Optional
 
 import numpy as np
 
-from ._lib import MswError, check, lib
+from ._lib import DevReadsT, MswError, check, lib
 
 
 class FastqReader:
@@ -86,6 +86,82 @@ class FastqReader:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         lib().msw_fastq_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return {"lines": a.value, "reads": b.value, "errors": c.value}
+
+
+class GpuFastqReader:
+    """The GPU-side lane reader (msw_gfastq_*, BGZF files): inflate, CRC,
+    line split and record parse run on the context's GPU; next_batch()
+    returns the batch's device arrays (valid until the call after next) and,
+    for tests, ``host=True`` copies them back."""
+
+    def __init__(self, ctx, path: str, stride: int = 256, max_reads: int = 1 << 20, with_pos: bool = False,
+                 span_bytes: int = 0):
+        self.ctx, self.path, self.stride, self.with_pos = ctx, path, stride, with_pos
+        h = ctypes.c_void_p()
+        check(lib().msw_gfastq_open(ctx.handle, path.encode(), stride, max_reads, 1 if with_pos else 0,
+                                    span_bytes, ctypes.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            lib().msw_gfastq_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def next_batch(self, host: bool = True):
+        """-> DevReadsT, or with host=True (seqs u8[n, stride], lens u16[n][, pos i64[n]])."""
+        d = DevReadsT()
+        check(lib().msw_gfastq_next(self._h, None, ctypes.byref(d)))
+        if not host:
+            return d
+        n = int(d.n)
+        seqs = np.zeros((n, self.stride), np.uint8)
+        lens = np.zeros(n, np.uint16)
+        L = lib()
+        check(L.msw_synchronize(self.ctx.handle))  # the emit ran on the context's compute stream
+        if n:
+            check(L.msw_memcpy_d2h(self.ctx.handle, seqs.ctypes.data, d.reads, seqs.nbytes))
+            check(L.msw_memcpy_d2h(self.ctx.handle, lens.ctypes.data, d.read_len, lens.nbytes))
+        if self.with_pos:
+            pos = np.zeros(n, np.int64)
+            if n:
+                check(L.msw_memcpy_d2h(self.ctx.handle, pos.ctypes.data, d.pos, pos.nbytes))
+            return seqs, lens, pos
+        return seqs, lens
+
+    def stats(self) -> dict:
+        v = [ctypes.c_uint64() for _ in range(6)]
+        lib().msw_gfastq_stats(self._h, *[ctypes.byref(x) for x in v])
+        keys = ("lines", "reads", "errors", "bases", "bytes_in", "bytes_out")
+        return {k: x.value for k, x in zip(keys, v)}
+
+
+def bgzf_inflate(ctx, data: bytes) -> bytes:
+    """msw_bgzf_inflate: a whole BGZF file inflated on the GPU (host to host)."""
+    src = np.frombuffer(data, np.uint8)
+    cap = 0
+    # the trailers give the exact size: sum of ISIZE over the members
+    p = 0
+    while p + 18 <= len(data):
+        bsize = data[p + 16] | (data[p + 17] << 8)
+        cap += int.from_bytes(data[p + bsize + 1 - 4:p + bsize + 1], "little")
+        p += bsize + 1
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = ctypes.c_uint64()
+    check(lib().msw_bgzf_inflate(ctx.handle, src.ctypes.data if len(src) else None, len(data), out.ctypes.data,
+                                 cap, ctypes.byref(n)))
+    return out[:n.value].tobytes()
 
 
 def process_fastq_file_in_chunks(filepath: str, chunk_size_reads: int,

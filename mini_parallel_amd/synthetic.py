@@ -166,23 +166,26 @@ def config_shard(k: int, a: int, b: int) -> PairBatch:
 BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 
 
-def bgzf_compress(data: bytes, level: int = 1) -> bytes:
+def bgzf_compress(data: bytes, level: int = 1, strategy: int = 0, block: int = 0xFF00,
+                  eof_block: bool = True) -> bytes:
     """BGZF (bgzip's block gzip): a multi-member gzip of <= 64 KiB blocks whose
     'BC' extra field holds the block size, then the empty EOF block.  Any gzip
     reader (zcat, the reference's lane loader) reads it as one stream; the C++
-    reader inflates it block by block with libdeflate."""
+    reader inflates it block by block with libdeflate, the GPU lane reader
+    with msw_inflate.hip.  ``strategy`` is zlib's (Z_FIXED, Z_RLE, ...)."""
     import struct
     import zlib
     out = []
-    for k in range(0, len(data), 0xFF00):
-        chunk = data[k:k + 0xFF00]
-        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    for k in range(0, len(data), block):
+        chunk = data[k:k + block]
+        c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, strategy)
         cdata = c.compress(chunk) + c.flush()
         out.append(struct.pack("<4BIBBH2BHH", 0x1F, 0x8B, 8, 4, 0, 0, 0xFF, 6, ord("B"), ord("C"), 2,
                                len(cdata) + 25))
         out.append(cdata)
         out.append(struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
-    out.append(BGZF_EOF)
+    if eof_block:
+        out.append(BGZF_EOF)
     return b"".join(out)
 
 

@@ -98,15 +98,18 @@ def test_files_mode_compat(tmp_path, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bgzf", [False, True])
-def test_full_wgs_sw_and_resume(tmp_path, oracle, bgzf):
-    """--full-wgs --score-mode sw over gzip or BGZF lane files (BGZF: libdeflate
-    block inflate, several threads per file): per-file i64 sums equal the
-    oracle's, checkpoint/resume skips finished files."""
+@pytest.mark.parametrize("bgzf,gpu_inflate", [(False, "1"), (True, "0"), (True, "1")])
+def test_full_wgs_sw_and_resume(tmp_path, oracle, bgzf, gpu_inflate):
+    """--full-wgs --score-mode sw over gzip or BGZF lane files (BGZF: inflated
+    and parsed on the GPU -- msw_gfastq -- or, with MSW_GPU_INFLATE=0, by
+    libdeflate on several host threads per file; gzip always on the host):
+    per-file i64 sums and per-read records equal the oracle's,
+    checkpoint/resume skips finished files."""
     from mini_parallel_amd.synthetic import write_wgs_dataset
     ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=2, reads_per_lane=2, reads_per_file=1500, bgzf=bgzf)
     env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "2",
-           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "700", "WGS_RUN_ID": "t1"}
+           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "700", "WGS_RUN_ID": "t1",
+           "MSW_GPU_INFLATE": gpu_inflate, "MSW_GFASTQ_BATCH": "500", "MSW_GFASTQ_SPAN_MB": "1"}
     (tmp_path / "scores").mkdir()
     args = ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
             "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json"),
@@ -131,6 +134,7 @@ def test_full_wgs_sw_and_resume(tmp_path, oracle, bgzf):
               "cpu_cores_used", "parallel_files", "system_info", "gcups", "num_gpus", "host_cores"):
         assert k in rec, k
     assert rec["files_processed"] == 4 and rec["chunk_size"] == 700 and rec["gcups"] > 0
+    assert rec["gpu_inflate"] == (bgzf and gpu_inflate == "1")
     assert set(rec["system_info"]) == {"gpu_name", "gpu_memory_gb", "cpu_cores", "total_ram_gb"}
     ck = json.load(open(tmp_path / "checkpoint_t1.json"))
     assert ck["completed_files"] == 4
@@ -167,7 +171,8 @@ REC_T = np.dtype([("score", "<i4"), ("end_i", "<i2"), ("end_j", "<i2")])
 
 
 @pytest.mark.gpu
-def test_full_wgs_config4_shape_two_workers(tmp_path, oracle):
+@pytest.mark.parametrize("gpu_inflate", ["0", "1"])
+def test_full_wgs_config4_shape_two_workers(tmp_path, oracle, gpu_inflate):
     """BASELINE config 4's shape (8 lanes x R1/R2 lane files of 150 bp reads,
     300 bp windows), reduced to 2,000 reads per file, through the multi-worker
     path: MSW_DEVICES=0,0 --num-gpus 2 builds two contexts on the one GPU, so
@@ -179,7 +184,8 @@ def test_full_wgs_config4_shape_two_workers(tmp_path, oracle):
     ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=8, reads_per_lane=2, reads_per_file=2000, bgzf=True,
                            workers=4)
     env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "8",
-           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "600", "WGS_RUN_ID": "c4", "MSW_DEVICES": "0,0"}
+           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "600", "WGS_RUN_ID": "c4", "MSW_DEVICES": "0,0",
+           "MSW_GPU_INFLATE": gpu_inflate}
     (tmp_path / "scores").mkdir()
     args = ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
             "--num-gpus", "2", "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json"),
@@ -195,6 +201,7 @@ def test_full_wgs_config4_shape_two_workers(tmp_path, oracle):
     rec = json.load(open(tmp_path / "rec.json"))
     assert rec["total_score"] == sum(per_file) and rec["total_reads"] == 16 * 2000
     assert rec["num_gpus"] == 2 and rec["files_processed"] == 16
+    assert rec["gpu_inflate"] == (gpu_inflate == "1")
     for k in ("gcups", "gcups_end_to_end", "hbm_gbps", "roofline_fraction_hbm", "roofline_fraction_valu",
               "kernel_ms", "gpu_busy_fraction", "host_cpus_usable", "host_threads"):
         assert k in rec, k

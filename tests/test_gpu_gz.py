@@ -1,0 +1,258 @@
+"""GPU-side BGZF lane reader (msw_inflate.hip, msw_parse.hip, msw_gfastq.cpp).
+
+Oracles: zlib (the reference implementation of RFC 1951 inflate, via Python's
+zlib / gzip modules) for the inflated bytes, and the host reader
+(msw_fastq.cpp, itself checked against a restatement of aligner.rs:107-178 in
+tests/test_fastq.py) for the parsed reads.  Bit-exact comparisons throughout.
+"""
+import gzip
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from mini_parallel_amd import MswError
+from mini_parallel_amd.fastq import FastqReader, GpuFastqReader, bgzf_inflate
+from mini_parallel_amd.synthetic import bgzf_compress
+
+pytestmark = pytest.mark.gpu
+
+
+def fib_text(n_syms: int, seed: int) -> bytes:
+    """Symbol k appears fib(k) times: a skewed distribution whose Huffman code
+    reaches zlib's 15-bit length limit (with Z_HUFFMAN_ONLY)."""
+    f = [1, 1]
+    while len(f) < n_syms:
+        f.append(f[-1] + f[-2])
+    data = np.concatenate([np.full(c, 33 + k, np.uint8) for k, c in enumerate(f)])
+    np.random.default_rng(seed).shuffle(data)
+    return data.tobytes()
+
+
+def fastq_text(n: int, seed: int, qual="mixed", crlf=False) -> bytes:
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        m = int(rng.integers(60, 256))
+        seq = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), m))
+        if qual == "mixed":
+            q = bytes(rng.choice(np.frombuffer(b"#,:F", np.uint8), m, p=[0.02, 0.08, 0.2, 0.7]))
+        else:
+            q = b"I" * m
+        out.append(b"@SYN:%d:%d pos=%d\n%s\n+\n%s\n" % (i // 1000, i, int(rng.integers(0, 1 << 30)), seq, q))
+    t = b"".join(out)
+    return t.replace(b"\n", b"\r\n") if crlf else t
+
+
+def payloads():
+    rng = np.random.default_rng(7)
+    rnd = rng.integers(0, 256, 300_000, dtype=np.uint8).tobytes()
+    chunk = rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()
+    periodic = b"".join(bytes(rng.integers(65, 91, p, dtype=np.uint8)) * (3000 // p) for p in (1, 2, 3, 5, 17, 64, 250, 300))
+    return {
+        "fastq_l1": (fastq_text(3000, 1), 1, 0),
+        "fastq_l6": (fastq_text(3000, 2), 6, 0),
+        "fastq_l9": (fastq_text(3000, 3), 9, 0),
+        "random_l6_stored": (rnd, 6, 0),
+        "level0_stored": (fastq_text(500, 4), 0, 0),
+        "fixed_huffman": (fastq_text(1000, 5), 6, zlib.Z_FIXED),
+        "rle": (fastq_text(1000, 6), 6, zlib.Z_RLE),
+        "huffman_only": (fastq_text(1000, 8), 6, zlib.Z_HUFFMAN_ONLY),
+        "long_codes": (fib_text(22, 9), 6, zlib.Z_HUFFMAN_ONLY),
+        "runs_258": (b"A" * 200_000 + b"AC" * 50_000, 9, 0),
+        "far_matches": (chunk * 40, 9, 0),
+        "periodic_overlaps": (periodic, 9, 0),
+        "all_bytes": (bytes(range(256)) * 700, 6, 0),
+        "empty": (b"", 6, 0),
+    }
+
+
+@pytest.mark.parametrize("name", list(payloads()))
+def test_inflate_matches_zlib(gpu_ctx, name):
+    data, level, strategy = payloads()[name]
+    blob = bgzf_compress(data, level, strategy)
+    assert gzip.decompress(blob) == data
+    assert bgzf_inflate(gpu_ctx, blob) == data
+
+
+def test_inflate_small_members_and_fixed_tables_after_dynamic(gpu_ctx):
+    # many tiny members (thousands of waves), alternating block types inside a member
+    data = fastq_text(2000, 11)
+    blob = bgzf_compress(data, 6, 0, block=700)
+    assert bgzf_inflate(gpu_ctx, blob) == data
+    # one member whose deflate stream mixes block types: a long dynamic block,
+    # short flushed blocks (zlib emits them with the fixed code), incompressible
+    # bytes (stored), and the empty stored blocks of Z_SYNC_FLUSH
+    rnd = np.random.default_rng(3).integers(0, 256, 3000, dtype=np.uint8).tobytes()
+    segs = [(data[:20000], zlib.Z_FULL_FLUSH), (b"AC", zlib.Z_FULL_FLUSH), (rnd, zlib.Z_SYNC_FLUSH),
+            (b"GATTACA", zlib.Z_SYNC_FLUSH), (data[20000:40000], zlib.Z_FULL_FLUSH), (b"T" * 600, zlib.Z_FINISH)]
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    raw, plain = b"", b""
+    for seg, fl in segs:
+        raw += c.compress(seg) + c.flush(fl)
+        plain += seg
+    member = struct.pack("<4BIBBH2BHH", 0x1F, 0x8B, 8, 4, 0, 0, 0xFF, 6, ord("B"), ord("C"), 2, len(raw) + 25) + raw \
+        + struct.pack("<II", zlib.crc32(plain) & 0xFFFFFFFF, len(plain))
+    assert len(plain) <= 65536 and gzip.decompress(member) == plain
+    assert bgzf_inflate(gpu_ctx, member) == plain
+
+
+def test_inflate_large_many_spans(gpu_ctx):
+    data = fastq_text(60_000, 12) * 2  # ~40 MB: thousands of members in one launch
+    blob = bgzf_compress(data, 6)
+    assert bgzf_inflate(gpu_ctx, blob) == data
+
+
+def test_inflate_errors(gpu_ctx):
+    data = fastq_text(400, 13)
+    blob = bytearray(bgzf_compress(data, 6))
+    # CRC trailer of the first member
+    bsize = blob[16] | (blob[17] << 8)
+    bad = bytearray(blob)
+    bad[bsize + 1 - 8] ^= 0x01
+    with pytest.raises(MswError, match="incorrect data check"):
+        bgzf_inflate(gpu_ctx, bytes(bad))
+    # ISIZE larger than the data
+    bad = bytearray(blob)
+    bad[bsize + 1 - 4] ^= 0x01
+    with pytest.raises(MswError):
+        bgzf_inflate(gpu_ctx, bytes(bad))
+    # corrupted deflate bytes: some error (zlib agrees the member is bad)
+    for off in (20, 40, 200, bsize - 40):
+        bad = bytearray(blob)
+        bad[off] ^= 0xA5
+        try:
+            ok = gzip.decompress(bytes(bad)) == data
+        except Exception:
+            ok = False
+        if not ok:
+            with pytest.raises(MswError):
+                bgzf_inflate(gpu_ctx, bytes(bad))
+    # truncated file
+    with pytest.raises(MswError):
+        bgzf_inflate(gpu_ctx, bytes(blob[:bsize - 5]))
+    # plain gzip is not BGZF
+    with pytest.raises(MswError, match="BGZF"):
+        bgzf_inflate(gpu_ctx, gzip.compress(data))
+
+
+# ---------------------------------------------------------------------------
+# The lane reader: GPU parse == host reader, record by record
+# ---------------------------------------------------------------------------
+def host_reads(path, stride=256):
+    seqs, lens, pos = [], [], []
+    with FastqReader(path) as fq:
+        while True:
+            s, ln, p = fq.next_chunk(5000, stride, with_pos=True)
+            if len(ln) == 0:
+                break
+            seqs.append(s)
+            lens.append(ln)
+            pos.append(p)
+        st = fq.stats()
+    if not seqs:
+        return np.zeros((0, stride), np.uint8), np.zeros(0, np.uint16), np.zeros(0, np.int64), st
+    return np.concatenate(seqs), np.concatenate(lens), np.concatenate(pos), st
+
+
+def gpu_reads(ctx, path, stride=256, max_reads=3000, span=1 << 20):
+    seqs, lens, pos = [], [], []
+    with GpuFastqReader(ctx, path, stride, max_reads, with_pos=True, span_bytes=span) as g:
+        first = 0
+        while True:
+            s, ln, p = g.next_batch()
+            if len(ln) == 0:
+                break
+            seqs.append(s)
+            lens.append(ln)
+            pos.append(p)
+            first += len(ln)
+        st = g.stats()
+    if not seqs:
+        return np.zeros((0, stride), np.uint8), np.zeros(0, np.uint16), np.zeros(0, np.int64), st
+    return np.concatenate(seqs), np.concatenate(lens), np.concatenate(pos), st
+
+
+def assert_reader_parity(ctx, path, **kw):
+    hs, hl, hp, hst = host_reads(path)
+    gs, gl, gp, gst = gpu_reads(ctx, path, **kw)
+    assert len(hl) == len(gl)
+    assert np.array_equal(hl, gl)
+    assert np.array_equal(hp, gp)
+    assert np.array_equal(hs, gs)
+    assert gst["reads"] == hst["reads"] and gst["lines"] == hst["lines"] and gst["errors"] == hst["errors"]
+    assert gst["bases"] == int(hl.astype(np.int64).sum())
+    return len(hl)
+
+
+@pytest.mark.parametrize("block", [0xFF00, 1000])
+@pytest.mark.parametrize("crlf", [False, True])
+def test_reader_matches_host_reader(gpu_ctx, tmp_path, block, crlf):
+    data = fastq_text(20_000, 21 + block % 7, crlf=crlf)  # ~7-8 MB: several 1 MiB spans, records straddle them
+    p = tmp_path / "lane.fastq.gz"
+    p.write_bytes(bgzf_compress(data, 6, block=block))
+    n = assert_reader_parity(gpu_ctx, str(p))
+    assert n == 20_000
+
+
+def test_reader_edge_files(gpu_ctx, tmp_path):
+    rng = np.random.default_rng(5)
+    cases = {
+        "empty": b"",
+        "no_final_newline": fastq_text(50, 1)[:-1],
+        "only_headers": b"@a pos=1\n",
+        "seq_at_eof": b"@a pos=12\nACGT",
+        "blank_lines": b"\n\n\n\n@x pos=3\nAC\n+\nII\n\n\n",
+        "pos_forms": b"@q pos=x pos=-7\nA\n+\nI\n@r pos=\nC\n+\nI\n@s pos=123456789012\nG\n+\nI\n@t\nT\n+\nI\n",
+        "len0_and_256": b"@a pos=1\n\n+\n\n@b pos=2\n" + b"A" * 256 + b"\n+\n" + b"I" * 256 + b"\n",
+        "utf8_valid_multibyte": "@é中 pos=9\nACGT\n+\néééé\n".encode() * 20,
+    }
+    for name, data in cases.items():
+        p = tmp_path / f"{name}.fastq.gz"
+        p.write_bytes(bgzf_compress(data, 6, block=int(rng.integers(5, 200))))
+        assert_reader_parity(gpu_ctx, str(p))
+    # a file holding only the BGZF EOF block
+    p = tmp_path / "eof_only.fastq.gz"
+    p.write_bytes(bgzf_compress(b"", 6))
+    assert_reader_parity(gpu_ctx, str(p))
+
+
+def test_reader_invalid_utf8_lines(gpu_ctx, tmp_path):
+    base = fastq_text(4000, 31).split(b"\n")
+    # ten invalid lines spread over the file (<= 10: skipped, not counted)
+    for k in range(10):
+        i = 37 + 997 * k
+        base[i] = b"\xff\xfe" + base[i]
+    data = b"\n".join(base)
+    p = tmp_path / "bad10.fastq.gz"
+    p.write_bytes(bgzf_compress(data, 6, block=3000))
+    assert_reader_parity(gpu_ctx, str(p))
+    # an eleventh one fails the file, with the host reader's message
+    base[3900] = b"\xc0\xaf" + base[3900]
+    p2 = tmp_path / "bad11.fastq.gz"
+    p2.write_bytes(bgzf_compress(b"\n".join(base), 6, block=3000))
+    with pytest.raises(MswError) as eh:
+        host_reads(str(p2))
+    with pytest.raises(MswError) as eg:
+        gpu_reads(gpu_ctx, str(p2))
+    assert str(eg.value) == str(eh.value)
+
+
+def test_reader_too_long_sequence(gpu_ctx, tmp_path):
+    data = fastq_text(100, 41) + b"@long pos=1\n" + b"A" * 300 + b"\n+\n" + b"I" * 300 + b"\n"
+    p = tmp_path / "long.fastq.gz"
+    p.write_bytes(bgzf_compress(data, 6))
+    with pytest.raises(MswError) as eh:
+        host_reads(str(p))
+    with pytest.raises(MswError) as eg:
+        gpu_reads(gpu_ctx, str(p))
+    assert eh.value.code == eg.value.code == -2  # MSW_E_RANGE
+
+
+def test_reader_rejects_plain_gzip(gpu_ctx, tmp_path):
+    p = tmp_path / "plain.fastq.gz"
+    p.write_bytes(gzip.compress(fastq_text(10, 1)))
+    with pytest.raises(MswError, match="BGZF"):
+        GpuFastqReader(gpu_ctx, str(p))
