@@ -90,7 +90,12 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
  * compute stream) -- scoring launched after it on that stream sees it.  The
  * device arrays stay valid until the call after next (two slabs alternate). */
 int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out);
-/* lines (valid), reads, errors (invalid lines), bases, compressed and inflated bytes so far */
+/* Point an open reader at another lane file (same context, stride, batch
+ * size and span): the device and pinned buffers are kept, so a worker that
+ * walks many files allocates once.  Batches of the previous file must not be
+ * used after the first msw_gfastq_next on the new one returns. */
+int msw_gfastq_reset(msw_gfastq* g, const char* path);
+/* lines (valid), reads, errors (invalid lines), bases, compressed and inflated bytes so far (this file) */
 void msw_gfastq_stats(const msw_gfastq* g, uint64_t* lines, uint64_t* reads, uint64_t* errors, uint64_t* bases,
                       uint64_t* bytes_in, uint64_t* bytes_out);
 void msw_gfastq_close(msw_gfastq* g);

@@ -604,8 +604,14 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
             chunk, strtoull(env_or("MSW_GFASTQ_BATCH", std::to_string(1u << 20)).c_str(), nullptr, 10));
         std::atomic<size_t> next_file{0};
         std::vector<std::thread> workers;
-        for (int gi = 0; gi < ngpu; ++gi) {
-            workers.emplace_back([&, gi]() {
+        // two workers (contexts) per GPU by default: one file's inflate and
+        // host reads overlap the other's scoring
+        const int per_gpu = std::max(1, atoi(env_or("MSW_GFASTQ_WORKERS_PER_GPU", "2").c_str()));
+        const int nworkers = ngpu * per_gpu;
+        gstats.assign((size_t)nworkers, msw_stats_t{});
+        for (int wi = 0; wi < nworkers; ++wi) {
+            workers.emplace_back([&, wi]() {
+                const int gi = wi % ngpu;
                 Ctx ctx(devices[gi].ordinal);
                 const msw_scoring_t sc = scoring_of(a);
                 msw_genome* gen = nullptr;
@@ -674,6 +680,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     }
                 };
                 int cur = 0;
+                msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
                 for (;;) {
                     const size_t k = next_file.fetch_add(1);
                     if (k >= todo.size()) break;
@@ -690,18 +697,21 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     }
                     printf("  Processing file %zu/%zu: %s (GPU inflate)\n", fi + 1, files.size(), f.path.c_str());
                     fflush(stdout);
-                    msw_gfastq* gr = nullptr;
-                    if (msw_gfastq_open(ctx.h, f.path.c_str(), kReadStride, batch, 1, 0, &gr) != MSW_OK) {
+                    const int orc = gr ? msw_gfastq_reset(gr, f.path.c_str())
+                                       : msw_gfastq_open(ctx.h, f.path.c_str(), kReadStride, batch, 1, 0, &gr);
+                    bool ok = orc == MSW_OK;
+                    if (!ok) {
                         f.error = msw_last_error();
                         fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
                         f.failed = true;
                     }
-                    while (gr) {
+                    while (ok) {
                         msw_dev_reads_t d;
                         if (msw_gfastq_next(gr, nullptr, &d) != MSW_OK) {
                             f.error = msw_last_error();
                             fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
                             f.failed = true;
+                            ok = false;
                             break;
                         }
                         if (d.n == 0) break;
@@ -734,10 +744,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         gz_in += bi;
                         gz_out += bo;
                     }
-                    msw_gfastq_close(gr);
                     f.reader_done = true;
                     finish_file(fi);
                 }
+                msw_gfastq_close(gr);
                 for (Res& r : res) {
                     msw_dev_free(ctx.h, r.d_score);
                     msw_dev_free(ctx.h, r.d_ei);
@@ -746,8 +756,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     msw_host_free(r.h);
                 }
                 msw_genome_destroy(gen);
-                msw_ctx_stats(ctx.h, &gstats[(size_t)gi], 0);
-                gstats[(size_t)gi].alg_bytes = alg_local;
+                msw_ctx_stats(ctx.h, &gstats[(size_t)wi], 0);
+                gstats[(size_t)wi].alg_bytes = alg_local;
             });
         }
         for (auto& t : workers) t.join();
@@ -758,7 +768,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         rep.wall_ms = ms_since(t_all);
         rep.cells = cells.load();
         rep.readers = 0;
-        rep.host_threads = ngpu;
+        rep.host_threads = nworkers;
         rep.gpu = gstats;
         rep.gpu_inflate = true;
         for (size_t i = 0; i < files.size(); ++i)

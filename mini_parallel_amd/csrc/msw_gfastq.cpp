@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -54,7 +55,8 @@ namespace {
 constexpr uint64_t kCarry = 64u << 10;     // room in front of a span for the previous span's last line
 constexpr uint64_t kPad = 256;             // device buffers: slack past the end for wide loads
 constexpr uint64_t kReadPiece = 8u << 20;  // compressed bytes per fread
-constexpr uint64_t kDefaultSpan = 256u << 20;
+constexpr uint64_t kInPad = 1024;          // past the compressed bytes: the inflate input window reads <= 520 B
+constexpr uint64_t kDefaultSpan = 1024u << 20;  // ~16k members: two rounds of 8 inflate waves per SIMD
 
 const char* status_text(uint32_t s) {
     switch (s) {
@@ -164,6 +166,7 @@ struct Inflater {
     uint32_t* d_flag = nullptr;             // [0] any error
     msw::GzCrcConsts* d_crc = nullptr;
     uint32_t* h_flag = nullptr;             // pinned
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // MSW_GZ_TIMING
 
     int init() {
         GZ_TRY(hipMalloc((void**)&d_flag, 64));
@@ -191,17 +194,38 @@ struct Inflater {
     int run(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, uint8_t* out,
             hipStream_t s) {
         int rc;
-        if ((rc = grow(&dc, &dc_cap, cbytes + 64))) return rc;
+        if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
         if ((rc = grow(&d_mem, &mem_cap, mem.size()))) return rc;
         if ((rc = grow(&d_status, &status_cap, mem.size()))) return rc;
         if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
-        GZ_TRY(hipMemsetAsync(dc + cbytes, 0, 64, s));
+        GZ_TRY(hipMemsetAsync(dc + cbytes, 0, kInPad, s));
         if (!mem.empty())
             GZ_TRY(hipMemcpyAsync(d_mem, mem.data(), mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
         GZ_TRY(hipMemsetAsync(d_flag, 0, 4, s));
         const uint32_t n = (uint32_t)mem.size();
+        static const bool timing = getenv("MSW_GZ_TIMING") != nullptr;  // kernel times to stderr (tools)
+        if (timing) {
+            if (!ev[0]) {
+                GZ_TRY(hipEventCreate(&ev[0]));
+                GZ_TRY(hipEventCreate(&ev[1]));
+                GZ_TRY(hipEventCreate(&ev[2]));
+            }
+            GZ_TRY(hipEventRecord(ev[0], s));
+        }
         GZ_TRY(msw::launch_gz_inflate(dc, d_mem, n, out, d_status, d_flag, s));
+        if (timing) GZ_TRY(hipEventRecord(ev[1], s));
         GZ_TRY(msw::launch_gz_crc(out, d_mem, n, d_crc, d_status, d_flag, s));
+        if (timing) {
+            GZ_TRY(hipEventRecord(ev[2], s));
+            GZ_TRY(hipEventSynchronize(ev[2]));
+            float a = 0, c = 0;
+            (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+            (void)hipEventElapsedTime(&c, ev[1], ev[2]);
+            uint64_t ob = 0;
+            for (const auto& m : mem) ob += m.isize;
+            fprintf(stderr, "[gz] %u members, %zu B in, %llu B out: inflate %.3f ms (%.2f GB/s out), crc %.3f ms\n", n,
+                    cbytes, (unsigned long long)ob, a, ob / (a * 1e6), c);
+        }
         GZ_TRY(hipMemcpyAsync(h_flag, d_flag, 4, hipMemcpyDeviceToHost, s));
         return MSW_OK;
     }
@@ -252,6 +276,7 @@ struct msw_gfastq {
     msw::ParseState* d_state = nullptr;
     msw::ParseOut* d_out = nullptr;
     msw::ParseOut* h_out = nullptr;  // pinned
+    msw::ParseState* h_state = nullptr;  // pinned
     msw::EmitSpan sp{};
 
     // batch slabs
@@ -289,6 +314,7 @@ void release(msw_gfastq* g) {
     if (g->d_state) (void)hipFree(g->d_state);
     if (g->d_out) (void)hipFree(g->d_out);
     if (g->h_out) (void)hipHostFree(g->h_out);
+    if (g->h_state) (void)hipHostFree(g->h_state);
     if (g->hc) (void)hipHostFree(g->hc);
     g->inf.release();
     if (g->parsed) (void)hipEventDestroy(g->parsed);
@@ -314,8 +340,14 @@ int fill_compressed(msw_gfastq* g, size_t want) {
 // Inflate and parse the next span into dout[next]; sets span_reads (0 is
 // possible: a span without a complete sequence line).  Returns MSW_OK with
 // at_eof set when the file has no more data.
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int next_span(msw_gfastq* g) {
     int rc;
+    static const bool trace = getenv("MSW_GFASTQ_TRACE") != nullptr;
+    const double t0 = trace ? now_ms() : 0.0;
     const int nx = g->cur < 0 ? 0 : 1 - g->cur;
     // 1. whole members whose output fits the span (compressed <= span bytes + 1 MiB)
     g->mem.clear();
@@ -337,6 +369,7 @@ int next_span(msw_gfastq* g) {
     if (g->fread_off >= g->fsize && used < g->hc_len && g->mem.empty())
         return set_error(MSW_E_INVALID, "Error reading %s: unexpected end of file", g->path.c_str());
 
+    const double t_read = trace ? now_ms() : 0.0;
     hipStream_t s = g->rs;
     // the buffer we write and the parse arrays are read by the previous span's emits
     if (g->emitted_valid) GZ_TRY(hipStreamWaitEvent(s, g->emitted, 0));
@@ -368,6 +401,7 @@ int next_span(msw_gfastq* g) {
     GZ_TRY(msw::launch_parse_a(b, s));
     GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
     GZ_TRY(hipStreamSynchronize(s));
+    const double t_a = trace ? now_ms() : 0.0;
     if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
     const uint64_t nlines = g->h_out->lines;
     const bool any_high = g->h_out->any_high != 0;
@@ -384,6 +418,11 @@ int next_span(msw_gfastq* g) {
     GZ_TRY(hipEventRecord(g->parsed, s));
     GZ_TRY(hipStreamSynchronize(s));
     const msw::ParseOut& o = *g->h_out;
+    if (trace)
+        fprintf(stderr, "[gfastq] %s span: %zu members, %.1f MB in, %.1f MB out: read+index %.2f ms, "
+                        "inflate+parse A %.2f ms, parse B %.2f ms, %llu reads\n",
+                g->path.c_str(), g->mem.size(), used / 1e6, obytes / 1e6, t_read - t0, t_a - t_read, now_ms() - t_a,
+                (unsigned long long)o.reads);
     if (o.err_over)
         return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
                          (unsigned long long)o.err_line);
@@ -414,6 +453,45 @@ int next_span(msw_gfastq* g) {
     g->errors += o.lines - o.valid;
     g->reads += o.reads;
     g->bases += o.bases;
+    return MSW_OK;
+}
+
+// Point the reader at a (new) lane file: per-file state back to the start,
+// buffers kept.  The parse state goes back to line 0 on the reader stream.
+int open_file(msw_gfastq* g, const char* path) {
+    if (g->f) fclose(g->f);
+    g->f = nullptr;
+    g->path = path;
+    g->fsize = g->fread_off = 0;
+    g->hc_len = 0;
+    g->cur = -1;
+    g->cur_off = g->cur_len = g->tail_start = 0;
+    g->started = g->at_eof = false;
+    g->span_reads = g->span_done = g->next_first = 0;
+    g->failed = 0;
+    g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
+    g->f = fopen(path, "rb");
+    if (!g->f) return set_error(MSW_E_INVALID, "Failed to open file %s", path);
+    fseeko(g->f, 0, SEEK_END);
+    g->fsize = (uint64_t)ftello(g->f);
+    fseeko(g->f, 0, SEEK_SET);
+    setvbuf(g->f, nullptr, _IONBF, 0);
+    if (g->fsize >= 18) {
+        uint8_t h[18];
+        if (fread(h, 1, 18, g->f) != 18 || member_size(h) < 26)
+            return set_error(MSW_E_INVALID, "%s is not a BGZF file", path);
+        fseeko(g->f, 0, SEEK_SET);
+    } else if (g->fsize > 0) {
+        return set_error(MSW_E_INVALID, "%s is not a BGZF file", path);
+    }
+    if (g->d_state) {
+        GZ_TRY(hipSetDevice(g->device));
+        if (g->emitted_valid) GZ_TRY(hipStreamWaitEvent(g->rs, g->emitted, 0));
+        const msw::ParseState st0{0, 0, -1, 0};
+        *g->h_state = st0;
+        GZ_TRY(hipMemcpyAsync(g->d_state, g->h_state, sizeof(st0), hipMemcpyHostToDevice, g->rs));
+        GZ_TRY(hipStreamSynchronize(g->rs));
+    }
     return MSW_OK;
 }
 
@@ -454,20 +532,6 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
         release(g);
         return rc;
     };
-    g->f = fopen(path, "rb");
-    if (!g->f) return bail(set_error(MSW_E_INVALID, "Failed to open file %s", path));
-    fseeko(g->f, 0, SEEK_END);
-    g->fsize = (uint64_t)ftello(g->f);
-    fseeko(g->f, 0, SEEK_SET);
-    setvbuf(g->f, nullptr, _IONBF, 0);
-    if (g->fsize >= 18) {
-        uint8_t h[18];
-        if (fread(h, 1, 18, g->f) != 18 || member_size(h) < 26)
-            return bail(set_error(MSW_E_INVALID, "%s is not a BGZF file", path));
-        fseeko(g->f, 0, SEEK_SET);
-    } else if (g->fsize > 0) {
-        return bail(set_error(MSW_E_INVALID, "%s is not a BGZF file", path));
-    }
     if (hipSetDevice(g->device) != hipSuccess) return bail(set_error(MSW_E_DEVICE, "hipSetDevice failed"));
     int rc;
     if ((rc = g->inf.init())) return bail(rc);
@@ -475,8 +539,9 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
         hipEventCreateWithFlags(&g->parsed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&g->emitted, hipEventDisableTiming) != hipSuccess)
         return bail(set_error(MSW_E_DEVICE, "stream/event creation failed"));
-    // compressed staging: a span of output is at most ~span compressed bytes (+ headers)
-    g->hc_cap = (size_t)(g->span + g->span / 8 + (4u << 20));
+    // compressed staging: half a span (FASTQ compresses ~3-4x; less
+    // compressible data just makes shorter spans) + room for one fread piece
+    g->hc_cap = (size_t)(std::max<uint64_t>(g->span / 2, 16u << 20) + kReadPiece + (1u << 20));
     if (hipHostMalloc((void**)&g->hc, g->hc_cap, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&g->h_out, sizeof(msw::ParseOut), hipHostMallocDefault) != hipSuccess)
         return bail(set_error(MSW_E_NOMEM, "hipHostMalloc failed (GPU lane reader staging)"));
@@ -490,13 +555,19 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
                                   (unsigned long long)(g->span >> 20)));
     }
     if (hipMalloc((void**)&g->d_state, sizeof(msw::ParseState)) != hipSuccess ||
-        hipMalloc((void**)&g->d_out, sizeof(msw::ParseOut)) != hipSuccess)
+        hipMalloc((void**)&g->d_out, sizeof(msw::ParseOut)) != hipSuccess ||
+        hipHostMalloc((void**)&g->h_state, sizeof(msw::ParseState), hipHostMallocDefault) != hipSuccess)
         return bail(set_error(MSW_E_NOMEM, "hipMalloc failed (GPU lane reader state)"));
-    msw::ParseState st0{0, 0, -1, 0};
-    if (hipMemcpy(g->d_state, &st0, sizeof(st0), hipMemcpyHostToDevice) != hipSuccess)
-        return bail(set_error(MSW_E_DEVICE, "state upload failed"));
+    if ((rc = open_file(g, path))) return bail(rc);
     *out = g;
     return MSW_OK;
+}
+
+int msw_gfastq_reset(msw_gfastq* g, const char* path) {
+    if (!g || !path) return set_error(MSW_E_INVALID, "reader/path is NULL");
+    const int rc = open_file(g, path);
+    if (rc) g->failed = rc;
+    return rc;
 }
 
 int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {
@@ -562,7 +633,8 @@ int msw_bgzf_inflate(msw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t* o
     int rc = inf.init();
     uint8_t* dout = nullptr;
     uint8_t* hstage = nullptr;
-    constexpr uint64_t kGroup = 256u << 20;  // output bytes per launch
+    const char* ge = getenv("MSW_GZ_GROUP_MB");  // output bytes per launch (tools/inflate_bench.py)
+    const uint64_t kGroup = (ge && atoll(ge) > 0 ? (uint64_t)atoll(ge) : 256u) << 20;
     uint64_t p = 0, total = 0;
     std::vector<msw::GzMember> mem;
     while (!rc && p < len) {

@@ -36,22 +36,43 @@
 namespace msw {
 namespace {
 
-constexpr uint32_t kRing = 4096;  // LDS window of the most recent output bytes
+constexpr uint32_t kRing = 2048;  // LDS window of the most recent output bytes
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kChunk = 256;  // flush unit: 64 lanes x 4 bytes
 
 // order of the code-length code lengths in a dynamic block header
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
+constexpr uint32_t kFastBits = 9;   // lit/len lookup: next 9 stream bits -> up to 3 literals or one symbol
+constexpr uint32_t kFastDBits = 7;  // distance lookup
+// lit/len entry: [3:0] bits consumed, [5:4] n literals (0 = one symbol in
+// [16:8]), bit 6 = code longer than kFastBits (or invalid): canonical decode
+constexpr uint32_t kFastLong = 0x40u;
+
+// ~5 KB per wave, so 8 waves fit a SIMD (32 per CU): the decode is a serial
+// latency chain per member and throughput comes from waves in flight.  The
+// code-length decode's scratch (lens, sym_c) lives in fast_ll, which is only
+// built after it.
 struct __align__(16) InflateLds {
     uint32_t ring32[kRing / 4];
+    union {
+        uint32_t fast_ll[1u << kFastBits];
+        struct {
+            uint16_t sym_c[20];  // code-length alphabet
+            uint8_t lens[320];   // code lengths of the block being built (<= 286 + 30)
+        } hdr;
+    } u;
+    uint16_t fast_d[1u << kFastDBits];  // [3:0] bits, [8:4] symbol, bit 15 = long
     uint16_t sym_ll[288];  // lit/len symbols sorted by (code length, symbol)
     uint16_t sym_d[32];    // distance symbols
-    uint16_t sym_c[20];    // code-length alphabet
-    uint8_t lens[320];     // code lengths of the block being built (<= 286 + 30)
 };
+static_assert(sizeof(InflateLds) <= 5120, "8 waves per SIMD need <= 5 KB of LDS per wave");
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
+// A call's result is divergent to the compiler; every control value of the
+// decode loop must stay wave-uniform (SGPRs, scalar branches), so results of
+// the out-of-line table builders go through readfirstlane.
+__device__ __forceinline__ bool uni_bool(bool b) { return __builtin_amdgcn_readfirstlane(b ? 1 : 0) != 0; }
 
 // zlib inftrees.c rules: kind 0 = code-length code (must be complete),
 // 1 = lit/len, 2 = distance (incomplete only as a single 1-bit code).
@@ -59,8 +80,8 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
 // lane L in 1..15 gets lim = (first[L] + count[L]) << (15 - L) and
 // bas = offs[L] - first[L]; other lanes lim = 0.  Returns false on an
 // over-subscribed or (disallowed) incomplete set.
-__device__ bool build_code(const uint8_t* lens, uint32_t n, uint16_t* syms, uint32_t& lim, int32_t& bas,
-                           int kind) {
+__device__ __noinline__ bool build_code(const uint8_t* lens, uint32_t n, uint16_t* syms, uint32_t& lim,
+                                        int32_t& bas, int kind) {
     const uint32_t lane = lane_id();
     uint32_t cnt = 0;
     for (uint32_t s0 = 0; s0 < n; s0 += 64) {
@@ -117,31 +138,115 @@ __device__ bool build_code(const uint8_t* lens, uint32_t n, uint16_t* syms, uint
     return true;
 }
 
-// The bit reader: stream bits LSB-first from a 64-bit buffer refilled with
-// aligned dwords (one prefetched ahead).  All fields are wave-uniform.
+// Lookup tables over the next kFastBits (lit/len) / kFastDBits (distance)
+// stream bits, built from the canonical (lim, bas) pairs: an entry holds up to
+// three literals whose codes all fit (sequence and quality letters of FASTQ
+// have 1-4 bit codes, so one LDS read usually yields two or three output
+// bytes), or one symbol, or the "long" flag for the ballot decode.  A code's
+// length is exact from its known bits: r < lim[L] depends only on r's top L bits.
+__device__ __noinline__ void build_fast(uint32_t lim_ll, int32_t bas_ll, uint32_t lim_d, int32_t bas_d,
+                                        InflateLds& S) {
+    const uint32_t lane = lane_id();
+    uint32_t ll[16], ld[16];
+    int32_t bl[16], bd[16];
+#pragma unroll
+    for (int L = 1; L <= 15; ++L) {
+        ll[L] = (uint32_t)__builtin_amdgcn_readlane((int)lim_ll, L);
+        bl[L] = __builtin_amdgcn_readlane(bas_ll, L);
+        ld[L] = (uint32_t)__builtin_amdgcn_readlane((int)lim_d, L);
+        bd[L] = __builtin_amdgcn_readlane(bas_d, L);
+    }
+    // one lit/len symbol from the low `known` bits of v: returns its length (0 = not determined)
+    auto dec = [&](uint32_t v, uint32_t known, uint32_t& sym) __attribute__((always_inline)) -> uint32_t {
+        const uint32_t r = __builtin_bitreverse32(v) >> 17;
+        uint32_t L = 0;
+        int32_t B = 0;
+#pragma unroll
+        for (int k = kFastBits; k >= 1; --k)
+            if ((uint32_t)k <= known && r < ll[k]) {
+                L = (uint32_t)k;
+                B = bl[k];
+            }
+        if (L) sym = S.sym_ll[(uint32_t)(B + (int32_t)(r >> (15 - L)))];
+        return L;
+    };
+    for (uint32_t i = lane; i < (1u << kFastBits); i += 64) {
+        uint32_t s1 = 0, e = kFastLong;
+        const uint32_t L1 = dec(i, kFastBits, s1);
+        if (L1) {
+            if (s1 >= 256) {
+                e = L1 | (s1 << 8);
+            } else {
+                uint32_t n = 1, used = L1, bytes = s1, s2 = 0;
+                const uint32_t L2 = dec(i >> used, kFastBits - used, s2);
+                if (L2 && s2 < 256) {
+                    bytes |= s2 << 8;
+                    ++n;
+                    used += L2;
+                    uint32_t s3 = 0;
+                    const uint32_t L3 = dec(i >> used, kFastBits - used, s3);
+                    if (L3 && s3 < 256) {
+                        bytes |= s3 << 16;
+                        ++n;
+                        used += L3;
+                    }
+                }
+                e = used | (n << 4) | (bytes << 8);
+            }
+        }
+        S.u.fast_ll[i] = e;
+    }
+    for (uint32_t i = lane; i < (1u << kFastDBits); i += 64) {
+        const uint32_t r = __builtin_bitreverse32(i) >> 17;
+        uint32_t L = 0;
+        int32_t B = 0;
+#pragma unroll
+        for (int k = kFastDBits; k >= 1; --k)
+            if (r < ld[k]) {
+                L = (uint32_t)k;
+                B = bd[k];
+            }
+        uint16_t e = 0x8000u;
+        if (L) e = (uint16_t)(L | ((uint32_t)S.sym_d[(uint32_t)(B + (int32_t)(r >> (15 - L)))] << 4));
+        S.fast_d[i] = e;
+    }
+    __syncthreads();
+}
+
+// The bit reader: stream bits LSB-first from a 64-bit buffer (wave-uniform)
+// refilled with dwords from a 64-dword window of the input held one per lane
+// in a VGPR (v_readlane).  The next window is loaded when this one runs out,
+// every 256 input bytes (~600 symbols): one memory latency there is ~1 % of
+// the decode, and nothing in the symbol loop waits on memory.
 struct Bits {
     const uint32_t* src;  // the span's compressed buffer as dwords
     uint64_t bb;
     uint32_t bcnt;        // valid bits in bb
-    uint32_t wi;          // dword index of nxt
-    uint32_t nxt;         // src[wi], loaded ahead
+    uint32_t wi;          // dword index of the next dword to merge
+    uint32_t wbase;       // dword index held by lane 0 of `cur`
+    uint32_t cur;         // per lane: src[wbase + lane]
     uint32_t wmax;        // refills past this dword index mean truncated data
 
     __device__ __forceinline__ void prime(uint64_t byte_pos) {
         const uint32_t w = (uint32_t)(byte_pos >> 2), sh = 8u * (uint32_t)(byte_pos & 3);
-        bb = (uint64_t)(src[w] >> sh);
+        wbase = w;
+        cur = src[w + lane_id()];
+        bb = (uint64_t)((uint32_t)__builtin_amdgcn_readlane((int)cur, 0) >> sh);
         bcnt = 32u - sh;
         wi = w + 1;
-        nxt = src[wi];
     }
     // true if the refill stayed within the member (+ slack)
     __device__ __forceinline__ bool refill() {
         if (bcnt < 32) {
-            bb |= (uint64_t)nxt << bcnt;
+            if (wi > wmax) return false;
+            if (wi - wbase >= 64) {
+                wbase = wi;
+                cur = src[wbase + lane_id()];
+            }
+            const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(wi - wbase));
+            bb |= (uint64_t)d << bcnt;
             bcnt += 32;
             ++wi;
-            if (wi > wmax) return false;
-            nxt = src[wi];
         }
         return true;
     }
@@ -176,7 +281,7 @@ __device__ __forceinline__ uint32_t coherent_load(const uint8_t* p) {
     return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(64) void gz_inflate_kernel(const uint8_t* __restrict__ cdata,
+__global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __restrict__ cdata,
                                                         const GzMember* __restrict__ members, uint32_t n,
                                                         uint8_t* __restrict__ out, uint32_t* __restrict__ status,
                                                         uint32_t* __restrict__ any_error) {
@@ -263,12 +368,13 @@ __global__ __launch_bounds__(64) void gz_inflate_kernel(const uint8_t* __restric
         if (btype == 1) {
             if (tables != 1) {
                 for (uint32_t s = lane; s < 288; s += 64)
-                    S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                    S.u.hdr.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
                 __syncthreads();
-                build_code(S.lens, 288, S.sym_ll, lim_ll, bas_ll, 1);
-                for (uint32_t s = lane; s < 32; s += 64) S.lens[s] = 5;
+                (void)uni_bool(build_code(S.u.hdr.lens, 288, S.sym_ll, lim_ll, bas_ll, 1));
+                for (uint32_t s = lane; s < 32; s += 64) S.u.hdr.lens[s] = 5;
                 __syncthreads();
-                build_code(S.lens, 32, S.sym_d, lim_d, bas_d, 2);
+                (void)uni_bool(build_code(S.u.hdr.lens, 32, S.sym_d, lim_d, bas_d, 2));
+                build_fast(lim_ll, bas_ll, lim_d, bas_d, S);
                 tables = 1;
             }
         } else {
@@ -276,33 +382,33 @@ __global__ __launch_bounds__(64) void gz_inflate_kernel(const uint8_t* __restric
             if (!br.refill()) { err = GZ_E_TRUNC; break; }
             const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
             if (nlen > 286 || ndist > 30) { err = GZ_E_HEADER; break; }
-            if (lane < 19) S.lens[lane] = 0;
+            if (lane < 19) S.u.hdr.lens[lane] = 0;
             __syncthreads();
             // code-length code lengths, 3 bits each, in kClOrder (RFC 1951 3.2.7)
             for (uint32_t i = 0; i < ncode; ++i) {
                 if (!br.refill()) { err = GZ_E_TRUNC; break; }
                 const uint32_t v = br.take(3);
-                if (lane == 0) S.lens[kClOrder[i]] = (uint8_t)v;
+                if (lane == 0) S.u.hdr.lens[kClOrder[i]] = (uint8_t)v;
             }
             if (err) break;
             __syncthreads();
-            if (!build_code(S.lens, 19, S.sym_c, lim_c, bas_c, 0)) { err = GZ_E_CODES; break; }
+            if (!uni_bool(build_code(S.u.hdr.lens, 19, S.u.hdr.sym_c, lim_c, bas_c, 0))) { err = GZ_E_CODES; break; }
             // lit/len + distance code lengths (one sequence; repeats may cross)
             const uint32_t total = nlen + ndist;
             uint32_t idx = 0;
             while (idx < total) {
                 if (!br.refill()) { err = GZ_E_TRUNC; break; }
-                const int sym = decode_sym(br, lim_c, bas_c, S.sym_c);
+                const int sym = decode_sym(br, lim_c, bas_c, S.u.hdr.sym_c);
                 if (sym < 0) { err = GZ_E_CODES; break; }
                 if (sym < 16) {
-                    if (lane == 0) S.lens[idx] = (uint8_t)sym;
+                    if (lane == 0) S.u.hdr.lens[idx] = (uint8_t)sym;
                     ++idx;
                     continue;
                 }
                 uint32_t rep, val = 0;
                 if (sym == 16) {
                     if (idx == 0) { err = GZ_E_HEADER; break; }
-                    val = __builtin_amdgcn_readfirstlane((uint32_t)S.lens[idx - 1]);
+                    val = __builtin_amdgcn_readfirstlane((uint32_t)S.u.hdr.lens[idx - 1]);
                     rep = 3 + br.take(2);
                 } else if (sym == 17) {
                     rep = 3 + br.take(3);
@@ -310,21 +416,43 @@ __global__ __launch_bounds__(64) void gz_inflate_kernel(const uint8_t* __restric
                     rep = 11 + br.take(7);
                 }
                 if (idx + rep > total) { err = GZ_E_HEADER; break; }
-                for (uint32_t k = lane; k < rep; k += 64) S.lens[idx + k] = (uint8_t)val;
+                for (uint32_t k = lane; k < rep; k += 64) S.u.hdr.lens[idx + k] = (uint8_t)val;
                 idx += rep;
             }
             if (err) break;
             __syncthreads();
-            if (S.lens[256] == 0) { err = GZ_E_CODES; break; }
-            if (!build_code(S.lens, nlen, S.sym_ll, lim_ll, bas_ll, 1)) { err = GZ_E_CODES; break; }
-            if (!build_code(S.lens + nlen, ndist, S.sym_d, lim_d, bas_d, 2)) { err = GZ_E_CODES; break; }
+            if (__builtin_amdgcn_readfirstlane((uint32_t)S.u.hdr.lens[256]) == 0) { err = GZ_E_CODES; break; }
+            if (!uni_bool(build_code(S.u.hdr.lens, nlen, S.sym_ll, lim_ll, bas_ll, 1))) { err = GZ_E_CODES; break; }
+            if (!uni_bool(build_code(S.u.hdr.lens + nlen, ndist, S.sym_d, lim_d, bas_d, 2))) { err = GZ_E_CODES; break; }
+            build_fast(lim_ll, bas_ll, lim_d, bas_d, S);
             tables = 2;
         }
         // Huffman-coded data until end-of-block
         for (;;) {
             if (!br.refill()) { err = GZ_E_TRUNC; break; }
-            const int sym = decode_sym(br, lim_ll, bas_ll, S.sym_ll);
-            if (sym < 0) { err = GZ_E_SYMBOL; break; }
+            const uint32_t e = __builtin_amdgcn_readfirstlane(S.u.fast_ll[(uint32_t)br.bb & ((1u << kFastBits) - 1u)]);
+            const uint32_t nlit = (e >> 4) & 3u;
+            if (nlit) {
+                // 1..3 literals from one lookup: lane k writes the k-th
+                if (opos + nlit > isize) { err = GZ_E_OVERRUN; break; }
+                if (lane < nlit) ring[(opos + lane) & kRingMask] = (uint8_t)(e >> (8 + 8 * lane));
+                br.drop(e & 15u);
+                const uint32_t before = opos;
+                opos += nlit;
+                if ((opos ^ before) & ~(kChunk - 1)) {
+                    flushed = opos & ~(kChunk - 1);
+                    flush_chunk(flushed - kChunk);
+                }
+                continue;
+            }
+            int sym;
+            if (e & kFastLong) {
+                sym = decode_sym(br, lim_ll, bas_ll, S.sym_ll);
+                if (sym < 0) { err = GZ_E_SYMBOL; break; }
+            } else {
+                sym = (int)((e >> 8) & 0x1FFu);
+                br.drop(e & 15u);
+            }
             if (sym < 256) {
                 if (opos >= isize) { err = GZ_E_OVERRUN; break; }
                 if (lane == 0) ring[opos & kRingMask] = (uint8_t)sym;
@@ -345,7 +473,15 @@ __global__ __launch_bounds__(64) void gz_inflate_kernel(const uint8_t* __restric
                 len = 258;
             }
             if (!br.refill()) { err = GZ_E_TRUNC; break; }
-            const int ds = decode_sym(br, lim_d, bas_d, S.sym_d);
+            const uint32_t ed = __builtin_amdgcn_readfirstlane(
+                (uint32_t)S.fast_d[(uint32_t)br.bb & ((1u << kFastDBits) - 1u)]);
+            int ds;
+            if (ed & 0x8000u) {
+                ds = decode_sym(br, lim_d, bas_d, S.sym_d);
+            } else {
+                ds = (int)((ed >> 4) & 31u);
+                br.drop(ed & 15u);
+            }
             if (ds < 0 || ds > 29) { err = GZ_E_SYMBOL; break; }
             uint32_t dist;
             if (ds < 4) {

@@ -163,9 +163,10 @@ __global__ __launch_bounds__(256) void k_count(ParseBufs b) {
     }
 }
 
-__global__ __launch_bounds__(1024) void k_scan_tiles(ParseBufs b) {
+// 256 threads: a single workgroup that fits on a CU beside inflate waves
+__global__ __launch_bounds__(256) void k_scan_tiles(ParseBufs b) {
     const uint32_t n = b.ntiles, t = threadIdx.x;
-    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t per = (n + 255) / 256;
     const uint32_t a = min(n, t * per), e = min(n, a + per);
     uint32_t s = 0, h = 0;
     for (uint32_t i = a; i < e; ++i) {
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(ParseBufs b) {
         h |= b.tile_hi[i];
     }
     uint32_t tot;
-    uint32_t pre = block_excl_scan<1024>(s, &tot);
+    uint32_t pre = block_excl_scan<256>(s, &tot);
     for (uint32_t i = a; i < e; ++i) {
         const uint32_t c = b.tile_nl[i];
         b.tile_nl[i] = pre;
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(256) void k_emit(ParseBufs b, EmitSpan sp, uint64_t
 hipError_t launch_parse_a(const ParseBufs& b, hipStream_t stream) {
     const uint32_t nt = b.ntiles ? b.ntiles : 1;
     hipLaunchKernelGGL(k_count, dim3(nt), dim3(256), 0, stream, b);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, b);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(256), 0, stream, b);
     return hipGetLastError();
 }
 

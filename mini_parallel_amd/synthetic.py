@@ -192,7 +192,7 @@ def bgzf_compress(data: bytes, level: int = 1, strategy: int = 0, block: int = 0
 def _write_lane_file(job):
     """One lane file of write_wgs_dataset (a process-pool job)."""
     import gzip
-    (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep, bgzf) = job
+    (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep, bgzf, qual) = job
     genome_bases = int(g.shape[0])
     b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_arr=g,
                    read_stride=(read_len + 16 + 15) // 16 * 16)
@@ -202,10 +202,25 @@ def _write_lane_file(job):
     span = genome_bases - int(b.win_len.max())
     pos = np.where(b.pos >= 0, np.minimum(b.pos, span), rng.integers(0, span, b.n_pairs))
     rl = b.read_len.astype(np.int64)
-    qual = b"I" * int(rl.max() if b.n_pairs else 0)
     tag = sample.encode()
+    if qual == "I":
+        q = b"I" * int(rl.max() if b.n_pairs else 0)
+        quals = [q[:rl[i]] for i in range(b.n_pairs)]
+    else:
+        # "binned": NovaSeq-style 4-level qualities; "illumina": 2..41 drifting
+        # down the read with noise (HiSeq-style, much less compressible)
+        tot = int(rl.sum())
+        if qual == "binned":
+            qb = rng.choice(np.frombuffer(b"F:,#", np.uint8), tot, p=[0.84, 0.11, 0.04, 0.01])
+        else:
+            cyc = np.concatenate([np.arange(int(m)) for m in rl]) if b.n_pairs else np.zeros(0, np.int64)
+            qv = 40 - cyc // 12 + rng.integers(-6, 3, tot)
+            qb = (np.clip(qv, 2, 41) + 33).astype(np.uint8)
+        ends = np.cumsum(rl)
+        raw = qb.tobytes()
+        quals = [raw[int(e - m):int(e)] for e, m in zip(ends, rl)]
     recs = [b"@%s:%d:%d pos=%d\n%s\n+\n%s\n" % (tag, lane, i, int(pos[i]), b.reads[i, :rl[i]].tobytes(),
-                                                  qual[:rl[i]]) for i in range(b.n_pairs)]
+                                                  quals[i]) for i in range(b.n_pairs)]
     if bgzf:
         with open(name, "wb") as f:
             f.write(bgzf_compress(b"".join(recs), compresslevel))
@@ -223,13 +238,15 @@ def _write_lane_file(job):
 def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_per_lane: int = 2,
                       reads_per_file: int = 1000, read_len: int = 150, win_factor: float = 2.0,
                       seed: int = 1004, genome_bases: int = 1 << 20, keep_batches: bool = True,
-                      compresslevel: int = 1, workers: int = 1, bgzf: bool = False) -> dict:
+                      compresslevel: int = 1, workers: int = 1, bgzf: bool = False, qual: str = "I") -> dict:
     """Config-4-shaped dataset: lane files {sample}_L{lane:03}_R{r}_001.fastq.gz
     (aligner.rs:198-204 naming) whose headers carry "pos=<window start>", and
     the reference genome as reference.fa.  Returns paths and (keep_batches) the
     pair batches (reads, windows) so tests can score them with the oracle.
     Vectorised, and ``workers`` > 1 writes the lane files in parallel processes
-    (same files either way).  ``bgzf`` writes block-gzip (bgzip) lane files."""
+    (same files either way).  ``bgzf`` writes block-gzip (bgzip) lane files;
+    ``qual`` picks the quality strings: "I" (constant), "binned" (NovaSeq
+    4-level) or "illumina" (Q2-Q41 drifting down the read, noisy)."""
     import os
     os.makedirs(out_dir, exist_ok=True)
     rng = np.random.default_rng(seed)
@@ -244,7 +261,7 @@ def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_p
         for r in range(1, reads_per_lane + 1):
             name = os.path.join(out_dir, "%s_L%03d_R%d_001.fastq.gz" % (sample, lane, r))
             jobs.append((g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel,
-                         keep_batches, bgzf))
+                         keep_batches, bgzf, qual))
             files.append(name)
             k += 1
     if workers > 1 and len(jobs) > 1:
