@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/msw.h"
@@ -212,8 +213,26 @@ struct Inflater {
             }
             GZ_TRY(hipEventRecord(ev[0], s));
         }
-        GZ_TRY(msw::launch_gz_inflate(dc, d_mem, n, out, d_status, d_flag, s));
+        static const bool prof_on = getenv("MSW_GZ_PROFILE") != nullptr;  // MSW_GZ_PROFILE builds: counters
+        uint32_t* d_prof = nullptr;
+        if (prof_on && n) GZ_TRY(hipMalloc((void**)&d_prof, (size_t)n * 64));
+        if (d_prof) GZ_TRY(hipMemsetAsync(d_prof, 0, (size_t)n * 64, s));
+        GZ_TRY(msw::launch_gz_inflate(dc, d_mem, n, out, d_status, d_flag, s, d_prof));
         if (timing) GZ_TRY(hipEventRecord(ev[1], s));
+        if (d_prof) {
+            std::vector<uint32_t> h((size_t)n * 16);
+            GZ_TRY(hipMemcpyAsync(h.data(), d_prof, h.size() * 4, hipMemcpyDeviceToHost, s));
+            GZ_TRY(hipStreamSynchronize(s));
+            double sum[12] = {0};
+            for (uint32_t m = 0; m < n; ++m)
+                for (int i = 0; i < 12; ++i) sum[i] += h[(size_t)m * 16 + i];
+            const char* names[12] = {"cycles", "hdr_cycles", "lit_iters", "lit_bytes", "sym_entries", "matches",
+                                     "far_matches", "refills", "flushes", "blocks", "copy_cycles", "-"};
+            fprintf(stderr, "[gzprof] per member:");
+            for (int i = 0; i < 11; ++i) fprintf(stderr, " %s=%.0f", names[i], sum[i] / n);
+            fprintf(stderr, "\n");
+            (void)hipFree(d_prof);
+        }
         GZ_TRY(msw::launch_gz_crc(out, d_mem, n, d_crc, d_status, d_flag, s));
         if (timing) {
             GZ_TRY(hipEventRecord(ev[2], s));
@@ -261,6 +280,12 @@ struct msw_gfastq {
     // compressed bytes read but not yet inflated: hc[0, hc_len)
     uint8_t* hc = nullptr;
     size_t hc_cap = 0, hc_len = 0;
+    // read-ahead: while the GPU inflates / the caller scores, a host thread
+    // reads the next span's compressed bytes into hc after hc_len
+    std::thread filler;
+    int fill_rc = 0;
+    std::string fill_msg;
+    size_t last_used = 0;
     Inflater inf;
     std::vector<msw::GzMember> mem;
 
@@ -295,7 +320,12 @@ struct msw_gfastq {
 
 namespace {
 
+void join_filler(msw_gfastq* g) {
+    if (g->filler.joinable()) g->filler.join();
+}
+
 void release(msw_gfastq* g) {
+    join_filler(g);
     if (g->f) fclose(g->f);
     (void)hipSetDevice(g->device);
     if (g->rs) (void)hipStreamSynchronize(g->rs);
@@ -340,6 +370,21 @@ int fill_compressed(msw_gfastq* g, size_t want) {
 // Inflate and parse the next span into dout[next]; sets span_reads (0 is
 // possible: a span without a complete sequence line).  Returns MSW_OK with
 // at_eof set when the file has no more data.
+int fill_compressed(msw_gfastq* g, size_t want);
+
+// Start reading ahead ~one span's compressed bytes (the last span's size) in
+// the background; next_span joins before it touches hc.
+void start_filler(msw_gfastq* g) {
+    join_filler(g);
+    if (g->fread_off >= g->fsize || g->hc_len >= g->hc_cap) return;
+    const size_t want = std::min(g->hc_cap, g->hc_len + g->last_used + kReadPiece);
+    g->fill_rc = 0;
+    g->filler = std::thread([g, want]() {
+        g->fill_rc = fill_compressed(g, want);
+        if (g->fill_rc) g->fill_msg = msw_last_error();  // thread-local: carried to the caller's thread
+    });
+}
+
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -349,6 +394,8 @@ int next_span(msw_gfastq* g) {
     static const bool trace = getenv("MSW_GFASTQ_TRACE") != nullptr;
     const double t0 = trace ? now_ms() : 0.0;
     const int nx = g->cur < 0 ? 0 : 1 - g->cur;
+    join_filler(g);
+    if (g->fill_rc) return set_error(g->fill_rc, "%s", g->fill_msg.c_str());
     // 1. whole members whose output fits the span (compressed <= span bytes + 1 MiB)
     g->mem.clear();
     size_t used = 0;
@@ -403,6 +450,13 @@ int next_span(msw_gfastq* g) {
     GZ_TRY(hipStreamSynchronize(s));
     const double t_a = trace ? now_ms() : 0.0;
     if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
+    // the upload of hc has completed: drop the consumed bytes and read ahead
+    if (used) {
+        memmove(g->hc, g->hc + used, g->hc_len - used);
+        g->hc_len -= used;
+    }
+    g->last_used = used;
+    start_filler(g);
     const uint64_t nlines = g->h_out->lines;
     const bool any_high = g->h_out->any_high != 0;
     // 5. size the line arrays, phase B
@@ -429,11 +483,6 @@ int next_span(msw_gfastq* g) {
     if (o.too_long)
         return set_error(MSW_E_RANGE, "sequence longer than the slab stride %u at line %llu", g->stride,
                          (unsigned long long)o.too_long_line);
-    // consumed compressed bytes leave the staging buffer
-    if (used) {
-        memmove(g->hc, g->hc + used, g->hc_len - used);
-        g->hc_len -= used;
-    }
     g->bytes_in += used;
     g->bytes_out += obytes;
     g->cur = nx;
@@ -459,6 +508,7 @@ int next_span(msw_gfastq* g) {
 // Point the reader at a (new) lane file: per-file state back to the start,
 // buffers kept.  The parse state goes back to line 0 on the reader stream.
 int open_file(msw_gfastq* g, const char* path) {
+    join_filler(g);
     if (g->f) fclose(g->f);
     g->f = nullptr;
     g->path = path;
@@ -469,6 +519,8 @@ int open_file(msw_gfastq* g, const char* path) {
     g->started = g->at_eof = false;
     g->span_reads = g->span_done = g->next_first = 0;
     g->failed = 0;
+    g->fill_rc = 0;
+    g->last_used = 0;
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
     g->f = fopen(path, "rb");
     if (!g->f) return set_error(MSW_E_INVALID, "Failed to open file %s", path);

@@ -31,13 +31,26 @@
 // Errors follow zlib's inflate (inftrees.c rules for code sets): any error
 // marks the member and stops its wave; no byte is ever written outside the
 // member's ISIZE bytes of output.
+#include <cstdlib>
+
 #include "msw_gz.h"
 
 namespace msw {
 namespace {
 
-constexpr uint32_t kRing = 2048;  // LDS window of the most recent output bytes
-constexpr uint32_t kRingMask = kRing - 1;
+constexpr int kDefaultRingKb = 8;
+
+// MSW_GZ_PROFILE builds (tools/build_variant.sh gzprof -DMSW_GZ_PROFILE=1):
+// per-member event counts and cycle stamps into prof[m * 16 ..].
+#ifndef MSW_GZ_PROFILE
+#define MSW_GZ_PROFILE 0
+#endif
+#if MSW_GZ_PROFILE
+#define GZP(i, v) (pc[i] += (v))
+#else
+#define GZP(i, v) ((void)0)
+#endif
+
 constexpr uint32_t kChunk = 256;  // flush unit: 64 lanes x 4 bytes
 
 // order of the code-length code lengths in a dynamic block header
@@ -49,12 +62,14 @@ constexpr uint32_t kFastDBits = 7;  // distance lookup
 // [16:8]), bit 6 = code longer than kFastBits (or invalid): canonical decode
 constexpr uint32_t kFastLong = 0x40u;
 
-// ~5 KB per wave, so 8 waves fit a SIMD (32 per CU): the decode is a serial
-// latency chain per member and throughput comes from waves in flight.  The
-// code-length decode's scratch (lens, sym_c) lives in fast_ll, which is only
-// built after it.
+// Tables: ~3 KB per wave.  The code-length decode's scratch (lens, sym_c)
+// lives in fast_ll, which is only built after it.  The output ring (the
+// kernel's RING template parameter) comes on top: deflate distances reach
+// 32 KiB, and FASTQ members use the whole range (a 64 KiB member of
+// synthetic reads: 38 % of matches within 2 KiB, 72 % within 8 KiB, 93 %
+// within 16 KiB); a match further back than the ring reads the flushed
+// output from L2, so the ring size trades waves per SIMD against L2 trips.
 struct __align__(16) InflateLds {
-    uint32_t ring32[kRing / 4];
     union {
         uint32_t fast_ll[1u << kFastBits];
         struct {
@@ -66,7 +81,7 @@ struct __align__(16) InflateLds {
     uint16_t sym_ll[288];  // lit/len symbols sorted by (code length, symbol)
     uint16_t sym_d[32];    // distance symbols
 };
-static_assert(sizeof(InflateLds) <= 5120, "8 waves per SIMD need <= 5 KB of LDS per wave");
+static_assert(sizeof(InflateLds) <= 3072, "inflate tables: <= 3 KB of LDS per wave");
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
 // A call's result is divergent to the compiler; every control value of the
@@ -281,15 +296,34 @@ __device__ __forceinline__ uint32_t coherent_load(const uint8_t* p) {
     return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __restrict__ cdata,
+// waves per SIMD the LDS allows (160 KB per CU) for a ring of RING bytes
+template <uint32_t RING>
+constexpr int inflate_waves() {
+    return (int)(160u * 1024u / (RING + 3072u) / 4u) > 8 ? 8 : (int)(160u * 1024u / (RING + 3072u) / 4u);
+}
+
+template <uint32_t RING>
+__global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(const uint8_t* __restrict__ cdata,
                                                         const GzMember* __restrict__ members, uint32_t n,
                                                         uint8_t* __restrict__ out, uint32_t* __restrict__ status,
-                                                        uint32_t* __restrict__ any_error) {
+                                                        uint32_t* __restrict__ any_error, uint32_t* __restrict__ prof) {
+    constexpr uint32_t kRing = RING, kRingMask = RING - 1;
+#if MSW_GZ_PROFILE
+    uint32_t pc[12] = {0};
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
+    static_assert((RING & (RING - 1)) == 0 && RING >= 1024, "ring: a power of two >= 1 KiB");
     __shared__ InflateLds S;
+    // the ring, then 64 per-lane dummy bytes: lane-conditional ring writes
+    // become unconditional writes whose inactive lanes hit their own dummy
+    // byte (a VALU select instead of exec-mask SALU work in the hot loop)
+    __shared__ uint32_t ring_words[RING / 4 + 16];
     const uint32_t m = blockIdx.x;
     if (m >= n) return;
     const uint32_t lane = lane_id();
-    uint8_t* ring = (uint8_t*)S.ring32;
+    uint8_t* ring = (uint8_t*)ring_words;
+    const uint32_t dummy = RING + lane;  // this lane's dummy byte
+    const uint32_t lit_shift = 8u + 8u * min(lane, 2u);
     const GzMember mem = members[m];
     uint8_t* dst = out + mem.ooff;
     const uint32_t isize = mem.isize;
@@ -307,7 +341,7 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
 
     // flush [from, from + 256) of the output (ring-resident) to HBM
     auto flush_chunk = [&](uint32_t from) __attribute__((always_inline)) {
-        const uint32_t v = S.ring32[((from + 4u * lane) & kRingMask) >> 2];
+        const uint32_t v = ring_words[((from + 4u * lane) & kRingMask) >> 2];
         uint8_t* d = dst + from + 4u * lane;
         if (dst_al4) {
             *(uint32_t*)d = v;
@@ -322,6 +356,10 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
     bool last = false;
     while (!last && err == GZ_OK) {
         if (!br.refill()) { err = GZ_E_TRUNC; break; }
+#if MSW_GZ_PROFILE
+        const uint64_t t_hdr = __builtin_amdgcn_s_memtime();
+#endif
+        GZP(9, 1);
         const uint32_t hdr = br.take(3);
         last = (hdr & 1u) != 0;
         const uint32_t btype = hdr >> 1;
@@ -427,25 +465,40 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
             build_fast(lim_ll, bas_ll, lim_d, bas_d, S);
             tables = 2;
         }
-        // Huffman-coded data until end-of-block
+        // Huffman-coded data until end-of-block.  Token loop with the next
+        // lookup issued before the current token's ring writes / copy, so its
+        // LDS latency overlaps them.  ISIZE is enforced where output leaves
+        // the ring (flush) and at the end; the ring absorbs an overrun.
+        auto lookup = [&]() __attribute__((always_inline)) -> uint32_t {
+            return S.u.fast_ll[(uint32_t)br.bb & ((1u << kFastBits) - 1u)];
+        };
+        auto flush_to = [&]() __attribute__((always_inline)) -> bool {
+            if (opos > isize) return false;
+            while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
+            return true;
+        };
+#if MSW_GZ_PROFILE
+        GZP(1, (uint32_t)(__builtin_amdgcn_s_memtime() - t_hdr));
+#endif
+        if (!br.refill()) { err = GZ_E_TRUNC; break; }
+        uint32_t ev = lookup();
         for (;;) {
-            if (!br.refill()) { err = GZ_E_TRUNC; break; }
-            const uint32_t e = __builtin_amdgcn_readfirstlane(S.u.fast_ll[(uint32_t)br.bb & ((1u << kFastBits) - 1u)]);
+            const uint32_t e = __builtin_amdgcn_readfirstlane(ev);
             const uint32_t nlit = (e >> 4) & 3u;
             if (nlit) {
                 // 1..3 literals from one lookup: lane k writes the k-th
-                if (opos + nlit > isize) { err = GZ_E_OVERRUN; break; }
-                if (lane < nlit) ring[(opos + lane) & kRingMask] = (uint8_t)(e >> (8 + 8 * lane));
+                GZP(2, 1);
+                GZP(3, nlit);
                 br.drop(e & 15u);
-                const uint32_t before = opos;
+                if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                ev = lookup();
+                ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
                 opos += nlit;
-                if ((opos ^ before) & ~(kChunk - 1)) {
-                    flushed = opos & ~(kChunk - 1);
-                    flush_chunk(flushed - kChunk);
-                }
+                if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
                 continue;
             }
             int sym;
+            GZP(4, 1);
             if (e & kFastLong) {
                 sym = decode_sym(br, lim_ll, bas_ll, S.sym_ll);
                 if (sym < 0) { err = GZ_E_SYMBOL; break; }
@@ -453,11 +506,12 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
                 sym = (int)((e >> 8) & 0x1FFu);
                 br.drop(e & 15u);
             }
-            if (sym < 256) {
-                if (opos >= isize) { err = GZ_E_OVERRUN; break; }
-                if (lane == 0) ring[opos & kRingMask] = (uint8_t)sym;
+            if (sym < 256) {  // a literal with a long code
+                if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                ev = lookup();
+                ring[lane == 0 ? (opos & kRingMask) : dummy] = (uint8_t)sym;
                 ++opos;
-                if ((opos & (kChunk - 1)) == 0) { flush_chunk(opos - kChunk); flushed = opos; }
+                if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
                 continue;
             }
             if (sym == 256) break;
@@ -467,8 +521,8 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
             if (sym < 265) {
                 len = (uint32_t)sym - 254;
             } else if (sym < 285) {
-                const uint32_t e = ((uint32_t)sym - 261) >> 2;
-                len = ((4u + (((uint32_t)sym - 265) & 3u)) << e) + 3u + br.take(e);
+                const uint32_t x = ((uint32_t)sym - 261) >> 2;
+                len = ((4u + (((uint32_t)sym - 265) & 3u)) << x) + 3u + br.take(x);
             } else {
                 len = 258;
             }
@@ -487,31 +541,42 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
             if (ds < 4) {
                 dist = (uint32_t)ds + 1;
             } else {
-                const uint32_t e = ((uint32_t)ds >> 1) - 1;
-                dist = ((2u + ((uint32_t)ds & 1u)) << e) + 1u + br.take(e);
+                const uint32_t x = ((uint32_t)ds >> 1) - 1;
+                dist = ((2u + ((uint32_t)ds & 1u)) << x) + 1u + br.take(x);
             }
             if (dist > opos) { err = GZ_E_DIST; break; }
-            if (opos + len > isize) { err = GZ_E_OVERRUN; break; }
+            if (!br.refill()) { err = GZ_E_TRUNC; break; }
+            ev = lookup();  // the next token's entry, in flight during the copy
+            GZP(5, 1);
+#if MSW_GZ_PROFILE
+            const uint64_t t_copy = __builtin_amdgcn_s_memtime();
+#endif
             if (dist + len <= kRing) {
                 // ring -> ring; the source is the `dist` bytes before opos,
                 // read modulo dist when the copy overlaps itself
-                const float rd = __builtin_amdgcn_rcpf((float)dist);
-                for (uint32_t j0 = 0; j0 < len; j0 += 64) {
-                    const uint32_t j = j0 + lane;
-                    uint32_t s = j;
-                    if (dist < len) {
+                if (dist >= len) {
+                    for (uint32_t j0 = 0; j0 < len; j0 += 64) {
+                        const uint32_t j = j0 + lane;
+                        const bool on = j < len;
+                        const uint8_t v = ring[on ? ((opos - dist + j) & kRingMask) : dummy];
+                        ring[on ? ((opos + j) & kRingMask) : dummy] = v;
+                    }
+                } else {
+                    const float rd = __builtin_amdgcn_rcpf((float)dist);
+                    for (uint32_t j0 = 0; j0 < len; j0 += 64) {
+                        const uint32_t j = j0 + lane;
                         int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
                         if (r < 0) r += (int32_t)dist;
                         if (r >= (int32_t)dist) r -= (int32_t)dist;
-                        s = (uint32_t)r;
+                        const bool on = j < len;
+                        const uint8_t v = ring[on ? ((opos - dist + (uint32_t)r) & kRingMask) : dummy];
+                        ring[on ? ((opos + j) & kRingMask) : dummy] = v;
                     }
-                    uint8_t v = 0;
-                    if (j < len) v = ring[(opos - dist + s) & kRingMask];
-                    if (j < len) ring[(opos + j) & kRingMask] = v;
                 }
             } else {
                 // further back than the ring: the flushed output in L2 (the
-                // source ends >= 3.5 KiB before opos, i.e. before `flushed`)
+                // source ends well before `flushed`)
+                GZP(6, 1);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
                 for (uint32_t j0 = 0; j0 < len; j0 += kChunk) {
                     const uint32_t j = j0 + 4u * lane;
@@ -525,12 +590,16 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
                     }
                 }
             }
+#if MSW_GZ_PROFILE
+            GZP(10, (uint32_t)(__builtin_amdgcn_s_memtime() - t_copy));
+#endif
             opos += len;
-            while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
+            if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
         }
     }
     if (err == GZ_OK) {
-        if (opos != isize) err = GZ_E_SIZE;
+        if (opos > isize) err = GZ_E_OVERRUN;
+        else if (opos != isize) err = GZ_E_SIZE;
         else if ((br.bit_pos() - mem.coff * 8u + 7u) / 8u > mem.clen) err = GZ_E_TRUNC;
     }
     if (err == GZ_OK) {
@@ -541,6 +610,13 @@ __global__ __launch_bounds__(64, 8) void gz_inflate_kernel(const uint8_t* __rest
         status[m] = err;
         if (err) atomicOr(any_error, 1u);
     }
+#if MSW_GZ_PROFILE
+    pc[0] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start);
+    if (prof && lane == 0)
+        for (int i = 0; i < 12; ++i) prof[m * 16 + i] = pc[i];
+#else
+    (void)prof;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -620,9 +696,23 @@ __global__ __launch_bounds__(64) void gz_crc_kernel(const uint8_t* __restrict__ 
 }  // namespace
 
 hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint32_t n, uint8_t* out,
-                             uint32_t* status, uint32_t* any_error, hipStream_t stream) {
+                             uint32_t* status, uint32_t* any_error, hipStream_t stream, uint32_t* prof) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gz_inflate_kernel, dim3(n), dim3(64), 0, stream, cdata, members, n, out, status, any_error);
+    // MSW_GZ_RING_KB: the output ring in LDS (tools/inflate_bench.py sweeps it)
+    static const int ring_kb = [] {
+        const char* e = getenv("MSW_GZ_RING_KB");
+        return e ? atoi(e) : kDefaultRingKb;
+    }();
+#define GZ_LAUNCH(R) hipLaunchKernelGGL(gz_inflate_kernel<R>, dim3(n), dim3(64), 0, stream, cdata, members, n, out, \
+                                         status, any_error, prof)
+    switch (ring_kb) {
+        case 2: GZ_LAUNCH(2048); break;
+        case 4: GZ_LAUNCH(4096); break;
+        case 16: GZ_LAUNCH(16384); break;
+        case 32: GZ_LAUNCH(32768); break;
+        default: GZ_LAUNCH(8192); break;
+    }
+#undef GZ_LAUNCH
     return hipGetLastError();
 }
 

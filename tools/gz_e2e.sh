@@ -13,7 +13,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 D=/tmp/msw_gz_e2e
 timeout -k 10 500 python3 tools/wgs_e2e.py --dir $D --reads-per-file "$N" --bgzf --qual "$Q" --level "$L" \
-  --workers 16 --host-threads 16 --extra-env "MSW_GPU_INFLATE=0;MSW_GPU_INFLATE=1" --out "$OUT/e2e.jsonl" \
+  --workers 16 --host-threads 16 --extra-env "${VARIANTS:-MSW_GPU_INFLATE=0;MSW_GPU_INFLATE=1}" --out "$OUT/e2e.jsonl" \
   > "$OUT/e2e.log" 2>"$OUT/e2e.err"
 echo "e2e done"
 cp $D/reference.fa /tmp/ref_gz.fa

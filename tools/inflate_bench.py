@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--qual", default="binned")
     ap.add_argument("--level", type=int, default=6)
     ap.add_argument("--members", default="1,16,256,1024,2534,8192")
+    ap.add_argument("--strategy", default="default", choices=["default", "huffman_only", "rle", "fixed", "stored"])
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401
@@ -29,7 +30,10 @@ def main():
     text = gzip.decompress(open(ds["files"][0], "rb").read())
     blk = 0xFF00
     one = [text[k:k + blk] for k in range(0, len(text) - blk, blk)]
-    members = [bgzf_compress(m, args.level, eof_block=False) for m in one]
+    strat = {"default": 0, "huffman_only": zlib.Z_HUFFMAN_ONLY, "rle": zlib.Z_RLE, "fixed": zlib.Z_FIXED,
+             "stored": 0}[args.strategy]
+    level = 0 if args.strategy == "stored" else args.level
+    members = [bgzf_compress(m, level, strat, eof_block=False) for m in one]
     ctx = Context(0)
     for n in [int(x) for x in args.members.split(",")]:
         blob = b"".join(members[k % len(members)] for k in range(n))
