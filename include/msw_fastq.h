@@ -83,7 +83,8 @@ int msw_is_bgzf(const char* path);
 /* read_stride: multiple of 16, <= 256 (longer sequences are MSW_E_RANGE);
  * max_reads: batch size (device slabs for two batches are allocated);
  * span_bytes: decompressed bytes inflated and parsed per step (0 = default
- * 256 MiB, env MSW_GFASTQ_SPAN_MB). */
+ * 1 GiB, env MSW_GFASTQ_SPAN_MB).  path may be NULL: the buffers are
+ * allocated now and msw_gfastq_reset names the first file. */
 int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64_t max_reads, int want_pos,
                     uint64_t span_bytes, msw_gfastq** out);
 /* The next batch, enqueued on `stream` (a hipStream_t; NULL = the context's

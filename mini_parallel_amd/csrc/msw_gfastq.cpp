@@ -562,7 +562,7 @@ int msw_is_bgzf(const char* path) {
 
 int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64_t max_reads, int want_pos,
                     uint64_t span_bytes, msw_gfastq** out) {
-    if (!ctx || !path || !out) return set_error(MSW_E_INVALID, "ctx/path/out is NULL");
+    if (!ctx || !out) return set_error(MSW_E_INVALID, "ctx/out is NULL");
     *out = nullptr;
     if (read_stride == 0 || read_stride % 16 || read_stride > 256)
         return set_error(MSW_E_INVALID, "read_stride %u must be a multiple of 16 in [16, 256]", read_stride);
@@ -570,7 +570,7 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     msw_gfastq* g = new msw_gfastq();
     g->ctx = ctx;
     g->device = msw_detail::ctx_device(ctx);
-    g->path = path;
+    g->path = path ? path : "";
     g->stride = read_stride;
     g->max_reads = max_reads;
     g->want_pos = want_pos != 0;
@@ -610,7 +610,8 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
         hipMalloc((void**)&g->d_out, sizeof(msw::ParseOut)) != hipSuccess ||
         hipHostMalloc((void**)&g->h_state, sizeof(msw::ParseState), hipHostMallocDefault) != hipSuccess)
         return bail(set_error(MSW_E_NOMEM, "hipMalloc failed (GPU lane reader state)"));
-    if ((rc = open_file(g, path))) return bail(rc);
+    if (path && (rc = open_file(g, path))) return bail(rc);
+    if (!path) g->failed = MSW_E_INVALID;  // buffers only: msw_gfastq_reset names the first file
     *out = g;
     return MSW_OK;
 }
@@ -626,7 +627,10 @@ int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {
     if (!g || !out) return set_error(MSW_E_INVALID, "reader/out is NULL");
     memset(out, 0, sizeof(*out));
     out->read_stride = g->stride;
-    if (g->failed) return set_error(g->failed, "Error reading %s: the reader failed earlier", g->path.c_str());
+    if (g->failed)
+        return set_error(g->failed, g->path.empty() ? "GPU lane reader: no file (msw_gfastq_reset first)"
+                                                    : "Error reading %s: the reader failed earlier",
+                         g->path.c_str());
     if (hipSetDevice(g->device) != hipSuccess) return set_error(MSW_E_DEVICE, "hipSetDevice failed");
     hipStream_t cs = stream ? (hipStream_t)stream : msw_detail::ctx_compute_stream(g->ctx);
     while (g->span_done == g->span_reads) {
@@ -686,7 +690,7 @@ int msw_bgzf_inflate(msw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t* o
     uint8_t* dout = nullptr;
     uint8_t* hstage = nullptr;
     const char* ge = getenv("MSW_GZ_GROUP_MB");  // output bytes per launch (tools/inflate_bench.py)
-    const uint64_t kGroup = (ge && atoll(ge) > 0 ? (uint64_t)atoll(ge) : 256u) << 20;
+    const uint64_t kGroup = (ge && atoll(ge) > 0 ? (uint64_t)atoll(ge) : 1024u) << 20;  // ~16k members: two waves per SIMD slot
     uint64_t p = 0, total = 0;
     std::vector<msw::GzMember> mem;
     while (!rc && p < len) {

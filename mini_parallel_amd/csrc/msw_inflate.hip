@@ -38,7 +38,7 @@
 namespace msw {
 namespace {
 
-constexpr int kDefaultRingKb = 8;
+constexpr int kDefaultRingKb = 2;  // best measured throughput (tools/inflate_bench.py, profiles/r02/gz)
 
 // MSW_GZ_PROFILE builds (tools/build_variant.sh gzprof -DMSW_GZ_PROFILE=1):
 // per-member event counts and cycle stamps into prof[m * 16 ..].
@@ -58,9 +58,27 @@ __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12
 
 constexpr uint32_t kFastBits = 9;   // lit/len lookup: next 9 stream bits -> up to 3 literals or one symbol
 constexpr uint32_t kFastDBits = 7;  // distance lookup
-// lit/len entry: [3:0] bits consumed, [5:4] n literals (0 = one symbol in
-// [16:8]), bit 6 = code longer than kFastBits (or invalid): canonical decode
+// lit/len entry: [3:0] bits consumed, [5:4] n literals (their bytes in
+// [31:8]); with n = 0: bit 6 = code longer than kFastBits or invalid
+// (canonical decode), bit 7 = a length code: base length [16:8], extra bits
+// [19:17]; neither = end of block.
 constexpr uint32_t kFastLong = 0x40u;
+constexpr uint32_t kFastMatch = 0x80u;
+// distance entry: [3:0] bits, [7:4] extra bits, [22:8] base distance,
+// bit 31 = code longer than kFastDBits or invalid
+constexpr uint32_t kFastDLong = 0x80000000u;
+
+__device__ __forceinline__ uint32_t len_base(uint32_t sym, uint32_t& extra) {
+    if (sym < 265) { extra = 0; return sym - 254; }
+    if (sym < 285) { extra = (sym - 261) >> 2; return ((4u + ((sym - 265) & 3u)) << extra) + 3u; }
+    extra = 0;
+    return 258;
+}
+__device__ __forceinline__ uint32_t dist_base(uint32_t d, uint32_t& extra) {
+    if (d < 4) { extra = 0; return d + 1; }
+    extra = (d >> 1) - 1;
+    return ((2u + (d & 1u)) << extra) + 1u;
+}
 
 // Tables: ~3 KB per wave.  The code-length decode's scratch (lens, sym_c)
 // lives in fast_ll, which is only built after it.  The output ring (the
@@ -77,11 +95,11 @@ struct __align__(16) InflateLds {
             uint8_t lens[320];   // code lengths of the block being built (<= 286 + 30)
         } hdr;
     } u;
-    uint16_t fast_d[1u << kFastDBits];  // [3:0] bits, [8:4] symbol, bit 15 = long
+    uint32_t fast_d[1u << kFastDBits];
     uint16_t sym_ll[288];  // lit/len symbols sorted by (code length, symbol)
     uint16_t sym_d[32];    // distance symbols
 };
-static_assert(sizeof(InflateLds) <= 3072, "inflate tables: <= 3 KB of LDS per wave");
+static_assert(sizeof(InflateLds) <= 3328, "inflate tables: <= 3.25 KB of LDS per wave");
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
 // A call's result is divergent to the compiler; every control value of the
@@ -189,8 +207,14 @@ __device__ __noinline__ void build_fast(uint32_t lim_ll, int32_t bas_ll, uint32_
         uint32_t s1 = 0, e = kFastLong;
         const uint32_t L1 = dec(i, kFastBits, s1);
         if (L1) {
-            if (s1 >= 256) {
-                e = L1 | (s1 << 8);
+            if (s1 == 256) {
+                e = L1;  // end of block
+            } else if (s1 >= 257 && s1 <= 285) {
+                uint32_t x;
+                const uint32_t base = len_base(s1, x);
+                e = L1 | kFastMatch | (base << 8) | (x << 17);
+            } else if (s1 >= 256) {
+                e = kFastLong;  // 286 / 287: the canonical decode reports it
             } else {
                 uint32_t n = 1, used = L1, bytes = s1, s2 = 0;
                 const uint32_t L2 = dec(i >> used, kFastBits - used, s2);
@@ -221,8 +245,15 @@ __device__ __noinline__ void build_fast(uint32_t lim_ll, int32_t bas_ll, uint32_
                 L = (uint32_t)k;
                 B = bd[k];
             }
-        uint16_t e = 0x8000u;
-        if (L) e = (uint16_t)(L | ((uint32_t)S.sym_d[(uint32_t)(B + (int32_t)(r >> (15 - L)))] << 4));
+        uint32_t e = kFastDLong;
+        if (L) {
+            const uint32_t d = S.sym_d[(uint32_t)(B + (int32_t)(r >> (15 - L)))];
+            if (d <= 29) {
+                uint32_t x;
+                const uint32_t base = dist_base(d, x);
+                e = L | (x << 4) | (base << 8);
+            }
+        }
         S.fast_d[i] = e;
     }
     __syncthreads();
@@ -265,6 +296,25 @@ struct Bits {
         }
         return true;
     }
+    // refill() for loops with a single exit: 0 or GZ_E_TRUNC, never a load past wmax
+    __device__ __forceinline__ uint32_t refill_code() {
+        uint32_t bad = 0;
+        if (bcnt < 32) {
+            if (wi > wmax) {
+                bad = GZ_E_TRUNC;
+            } else {
+                if (wi - wbase >= 64) {
+                    wbase = wi;
+                    cur = src[wbase + lane_id()];
+                }
+                const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(wi - wbase));
+                bb |= (uint64_t)d << bcnt;
+                bcnt += 32;
+                ++wi;
+            }
+        }
+        return bad;
+    }
     __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
     __device__ __forceinline__ void drop(uint32_t n) {
         bb >>= n;
@@ -299,7 +349,9 @@ __device__ __forceinline__ uint32_t coherent_load(const uint8_t* p) {
 // waves per SIMD the LDS allows (160 KB per CU) for a ring of RING bytes
 template <uint32_t RING>
 constexpr int inflate_waves() {
-    return (int)(160u * 1024u / (RING + 3072u) / 4u) > 8 ? 8 : (int)(160u * 1024u / (RING + 3072u) / 4u);
+    return (int)(160u * 1024u / (RING + 64u + (uint32_t)sizeof(InflateLds)) / 4u) > 8
+               ? 8
+               : (int)(160u * 1024u / (RING + 64u + (uint32_t)sizeof(InflateLds)) / 4u);
 }
 
 template <uint32_t RING>
@@ -483,112 +535,116 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
         if (!br.refill()) { err = GZ_E_TRUNC; break; }
         uint32_t ev = lookup();
         for (;;) {
-            const uint32_t e = __builtin_amdgcn_readfirstlane(ev);
-            const uint32_t nlit = (e >> 4) & 3u;
-            if (nlit) {
-                // 1..3 literals from one lookup: lane k writes the k-th
-                GZP(2, 1);
-                GZP(3, nlit);
-                br.drop(e & 15u);
-                if (!br.refill()) { err = GZ_E_TRUNC; break; }
-                ev = lookup();
-                ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
-                opos += nlit;
-                if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
-                continue;
+            uint32_t e = __builtin_amdgcn_readfirstlane(ev);
+            if ((e >> 4) & 3u) {
+                // Literal runs: a tight inner loop while the lookups yield
+                // literals (1..3 per entry: lane k writes the k-th).
+                // failures clear `ok`, which masks the next entry to "not a
+                // literal": the loop keeps one exit and a one-instruction test
+                uint32_t ok = ~0u, bad = 0;
+                do {
+                    const uint32_t nlit = (e >> 4) & 3u;
+                    GZP(2, 1);
+                    GZP(3, nlit);
+                    br.drop(e & 15u);
+                    if (br.bcnt < 32) {
+                        const uint32_t c = br.refill_code();
+                        if (c) { bad = c; ok = 0; }
+                    }
+                    ev = lookup();
+                    ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
+                    opos += nlit;
+                    if (opos - flushed >= kChunk && !flush_to()) { bad = GZ_E_OVERRUN; ok = 0; }
+                    e = __builtin_amdgcn_readfirstlane(ev) & ok;
+                } while (e & 0x30u);
+                if (bad) { err = bad; break; }
             }
-            int sym;
             GZP(4, 1);
-            if (e & kFastLong) {
-                sym = decode_sym(br, lim_ll, bas_ll, S.sym_ll);
-                if (sym < 0) { err = GZ_E_SYMBOL; break; }
-            } else {
-                sym = (int)((e >> 8) & 0x1FFu);
-                br.drop(e & 15u);
-            }
-            if (sym < 256) {  // a literal with a long code
-                if (!br.refill()) { err = GZ_E_TRUNC; break; }
-                ev = lookup();
-                ring[lane == 0 ? (opos & kRingMask) : dummy] = (uint8_t)sym;
-                ++opos;
-                if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
-                continue;
-            }
-            if (sym == 256) break;
-            if (sym > 285) { err = GZ_E_SYMBOL; break; }
-            // length: 257..264 -> 3..10, 265..284 -> base + extra bits, 285 -> 258
             uint32_t len;
-            if (sym < 265) {
-                len = (uint32_t)sym - 254;
-            } else if (sym < 285) {
-                const uint32_t x = ((uint32_t)sym - 261) >> 2;
-                len = ((4u + (((uint32_t)sym - 265) & 3u)) << x) + 3u + br.take(x);
+            if (e & kFastMatch) {
+                // a length code from the table: base + extra bits, no branching on the symbol
+                br.drop(e & 15u);
+                len = ((e >> 8) & 0x1FFu) + br.take((e >> 17) & 7u);
+            } else if (!(e & kFastLong)) {
+                br.drop(e & 15u);  // end of block
+                break;
             } else {
-                len = 258;
+                // a code longer than the table (or invalid): canonical decode
+                const int sym = decode_sym(br, lim_ll, bas_ll, S.sym_ll);
+                if (sym < 0 || sym > 285) { err = GZ_E_SYMBOL; break; }
+                if (sym < 256) {
+                    if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                    ev = lookup();
+                    ring[lane == 0 ? (opos & kRingMask) : dummy] = (uint8_t)sym;
+                    ++opos;
+                    if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
+                    continue;
+                }
+                if (sym == 256) break;
+                uint32_t x;
+                len = len_base((uint32_t)sym, x);
+                len += br.take(x);
             }
-            if (!br.refill()) { err = GZ_E_TRUNC; break; }
-            const uint32_t ed = __builtin_amdgcn_readfirstlane(
-                (uint32_t)S.fast_d[(uint32_t)br.bb & ((1u << kFastDBits) - 1u)]);
-            int ds;
-            if (ed & 0x8000u) {
-                ds = decode_sym(br, lim_d, bas_d, S.sym_d);
-            } else {
-                ds = (int)((ed >> 4) & 31u);
-                br.drop(ed & 15u);
+            // distance
+            if (br.bcnt < 32) {
+                const uint32_t c = br.refill_code();
+                if (c) { err = c; break; }
             }
-            if (ds < 0 || ds > 29) { err = GZ_E_SYMBOL; break; }
+            const uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[(uint32_t)br.bb & ((1u << kFastDBits) - 1u)]);
             uint32_t dist;
-            if (ds < 4) {
-                dist = (uint32_t)ds + 1;
+            if (!(ed & kFastDLong)) {
+                br.drop(ed & 15u);
+                dist = ((ed >> 8) & 0x7FFFu) + br.take((ed >> 4) & 15u);
             } else {
-                const uint32_t x = ((uint32_t)ds >> 1) - 1;
-                dist = ((2u + ((uint32_t)ds & 1u)) << x) + 1u + br.take(x);
+                const int ds = decode_sym(br, lim_d, bas_d, S.sym_d);
+                if (ds < 0 || ds > 29) { err = GZ_E_SYMBOL; break; }
+                uint32_t x;
+                dist = dist_base((uint32_t)ds, x);
+                dist += br.take(x);
             }
             if (dist > opos) { err = GZ_E_DIST; break; }
-            if (!br.refill()) { err = GZ_E_TRUNC; break; }
+            if (br.bcnt < 32) {
+                const uint32_t c = br.refill_code();
+                if (c) { err = c; break; }
+            }
             ev = lookup();  // the next token's entry, in flight during the copy
             GZP(5, 1);
 #if MSW_GZ_PROFILE
             const uint64_t t_copy = __builtin_amdgcn_s_memtime();
 #endif
             if (dist + len <= kRing) {
-                // ring -> ring; the source is the `dist` bytes before opos,
-                // read modulo dist when the copy overlaps itself
-                if (dist >= len) {
-                    for (uint32_t j0 = 0; j0 < len; j0 += 64) {
-                        const uint32_t j = j0 + lane;
-                        const bool on = j < len;
-                        const uint8_t v = ring[on ? ((opos - dist + j) & kRingMask) : dummy];
-                        ring[on ? ((opos + j) & kRingMask) : dummy] = v;
-                    }
-                } else {
-                    const float rd = __builtin_amdgcn_rcpf((float)dist);
-                    for (uint32_t j0 = 0; j0 < len; j0 += 64) {
-                        const uint32_t j = j0 + lane;
-                        int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
-                        if (r < 0) r += (int32_t)dist;
-                        if (r >= (int32_t)dist) r -= (int32_t)dist;
-                        const bool on = j < len;
-                        const uint8_t v = ring[on ? ((opos - dist + (uint32_t)r) & kRingMask) : dummy];
-                        ring[on ? ((opos + j) & kRingMask) : dummy] = v;
-                    }
-                }
+                // ring -> ring, 64 bytes per instruction pair; byte j copies
+                // source byte j mod dist (overlapping copies repeat the last
+                // `dist` bytes; j mod dist = j when dist >= len).  Inactive
+                // lanes move their dummy byte.
+                const float rd = __builtin_amdgcn_rcpf((float)dist);
+                uint32_t j0 = 0;
+                do {
+                    const uint32_t j = j0 + lane;
+                    int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
+                    r += r < 0 ? (int32_t)dist : 0;
+                    r -= r >= (int32_t)dist ? (int32_t)dist : 0;
+                    const bool on = j < len;
+                    const uint8_t v = ring[on ? ((opos - dist + (uint32_t)r) & kRingMask) : dummy];
+                    ring[on ? ((opos + j) & kRingMask) : dummy] = v;
+                    j0 += 64;
+                } while (j0 < len);
             } else {
                 // further back than the ring: the flushed output in L2 (the
                 // source ends well before `flushed`)
                 GZP(6, 1);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
-                for (uint32_t j0 = 0; j0 < len; j0 += kChunk) {
-                    const uint32_t j = j0 + 4u * lane;
-                    if (j < len) {
-                        const uint64_t q = mem.ooff + (uint64_t)(opos - dist + j);
-                        const uint8_t* a = out + (q & ~(uint64_t)3);
-                        const uint32_t lo = coherent_load(a), hi = coherent_load(a + 4);
-                        const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(q & 3));
-                        const uint32_t nb = min(4u, len - j);
-                        for (uint32_t b = 0; b < nb; ++b) ring[(opos + j + b) & kRingMask] = (uint8_t)(v >> (8 * b));
-                    }
-                }
+                // lane j fetches byte j (the dword holding it; a wave's 64
+                // bytes are a few coalesced lines) -- no per-lane loops
+                uint32_t j0 = 0;
+                do {
+                    const uint32_t j = j0 + lane;
+                    const bool on = j < len;
+                    const uint64_t q = mem.ooff + (uint64_t)(opos - dist + (on ? j : 0u));
+                    const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
+                    ring[on ? ((opos + j) & kRingMask) : dummy] = (uint8_t)(w >> (8u * (uint32_t)(q & 3)));
+                    j0 += 64;
+                } while (j0 < len);
             }
 #if MSW_GZ_PROFILE
             GZP(10, (uint32_t)(__builtin_amdgcn_s_memtime() - t_copy));
