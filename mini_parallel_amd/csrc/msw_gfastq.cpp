@@ -90,16 +90,8 @@ msw::GzCrcConsts crc_consts() {
     uint32_t p = 1u << 30;  // x^1
     c.x2n[0] = p;
     for (int n = 1; n < 32; ++n) c.x2n[n] = p = multmodp(p, p);
-    auto x2nmodp = [&](uint64_t n, unsigned k) {
-        uint32_t q = 1u << 31;
-        while (n) {
-            if (n & 1) q = multmodp(c.x2n[k & 31], q);
-            n >>= 1;
-            ++k;
-        }
-        return q;
-    };
-    for (int k = 0; k < 6; ++k) c.slice[k] = x2nmodp(1024ull << k, 3);
+    for (int i = 0; i < 4; ++i)
+        for (uint32_t v = 0; v < 256; ++v) c.adv[i][v] = multmodp(c.x2n[11], v << (8 * i));  // x^2048
     return c;
 }
 

@@ -39,10 +39,11 @@ enum GzStatus : uint32_t {
     GZ_E_CRC = 10,      // CRC-32 mismatch
 };
 
-// CRC-32 constants for the combine step (zlib's x^(2^k) mod p table), host-built.
+// CRC-32 constants (zlib's x^(2^k) mod p table and the 256-byte advance), host-built.
 struct GzCrcConsts {
-    uint32_t x2n[32];   // x^(2^k) mod p(x), reflected
-    uint32_t slice[6];  // x^(8 * 1024 * 2^k) mod p(x): shift by a 1 KiB * 2^k tree node
+    uint32_t x2n[32];       // x^(2^k) mod p(x), reflected
+    uint32_t adv[4][256];   // adv[i][v] = (v << 8i) * x^(8 * 256) mod p: a raw CRC state
+                            // advanced over 256 bytes, one byte of the state at a time
 };
 
 // Inflate every member of a span (one wave per member); status[m] set for each.

@@ -25,9 +25,11 @@
 //    completed 256-byte chunk is flushed to HBM with one coalesced store per
 //    lane; matches reaching further back than the ring read the flushed
 //    output from L2 (agent-scope loads after the flush stores have drained);
-//  * the CRC-32 check is a second kernel: each lane CRCs a 1 KiB slice of the
-//    member's output and the 64 slice CRCs are combined in a 6-level tree
-//    with GF(2) shift constants (zlib's crc32_combine).
+//  * the CRC-32 check is a second kernel: a wave reads the member's output
+//    in coalesced 256-byte chunks, lane l folds dword l of every chunk into
+//    its own state with a table-driven 256-byte advance, and the 64 lane
+//    states are combined in a 6-level tree with GF(2) shift constants
+//    (zlib's crc32_combine).
 // Errors follow zlib's inflate (inftrees.c rules for code sets): any error
 // marks the member and stops its wave; no byte is ever written outside the
 // member's ISIZE bytes of output.
@@ -699,47 +701,81 @@ __device__ uint32_t x2nmodp(const GzCrcConsts& c, uint64_t n, uint32_t k) {  // 
     return p;
 }
 
-__global__ __launch_bounds__(64) void gz_crc_kernel(const uint8_t* __restrict__ out,
-                                                    const GzMember* __restrict__ members, uint32_t n,
-                                                    const GzCrcConsts* __restrict__ consts,
-                                                    uint32_t* __restrict__ status, uint32_t* __restrict__ any_error) {
-    __shared__ uint32_t T[256];
-    const uint32_t m = blockIdx.x;
-    if (m >= n) return;
-    const uint32_t lane = lane_id();
-    for (uint32_t i = lane; i < 256; i += 64) {
-        uint32_t c = i;
-        for (int k = 0; k < 8; ++k) c = c & 1 ? (c >> 1) ^ kPoly : c >> 1;
-        T[i] = c;
-    }
+// One wave per member, four members per block (the advance tables are shared
+// in LDS).  The member is cut into 256-byte chunks aligned to its END (the
+// front of the first chunk is virtual zeros, which leave a raw CRC -- no
+// pre/post conditioning -- unchanged), and lane l owns bytes [4l, 4l + 4) of
+// every chunk, so each chunk is one coalesced load per wave.  Lane l's share
+// of the message (its dwords, zeros elsewhere) runs through the recurrence
+// t <- A(t ^ d) with A = advance over 256 bytes (a linear map: four table
+// lookups, no serial byte chain), which keeps every lane's state aligned to
+// the start of its dword; the last dword is not advanced, and the 64 lane
+// states are combined as consecutive dwords in a 6-level tree:
+// raw(X || Y) = raw(X) * x^(8|Y|) ^ raw(Y)   (zlib crc32_combine).
+constexpr uint32_t kCrcMembersPerBlock = 4;
+
+__global__ __launch_bounds__(256) void gz_crc_kernel(const uint8_t* __restrict__ out,
+                                                     const GzMember* __restrict__ members, uint32_t n,
+                                                     const GzCrcConsts* __restrict__ consts,
+                                                     uint32_t* __restrict__ status, uint32_t* __restrict__ any_error) {
+    __shared__ uint32_t A[4][256];
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) (&A[0][0])[i] = (&consts->adv[0][0])[i];
     __syncthreads();
-    if (status[m] != GZ_OK) return;  // inflate already failed
+    const uint32_t m = blockIdx.x * kCrcMembersPerBlock + (threadIdx.x >> 6);
+    if (m >= n || status[m] != GZ_OK) return;  // no barrier below; failed members stay failed
+    const uint32_t lane = threadIdx.x & 63;
     const GzMember mem = members[m];
-    // Virtual 64 KiB of output, zero-padded at the front (a raw CRC -- no
-    // pre/post conditioning -- of leading zeros is 0): lane l owns virtual
-    // bytes [1024 l, 1024 l + 1024), so every tree node has a power-of-two size.
-    const uint32_t pad = 65536u - mem.isize;
-    const uint32_t a = max(1024u * lane, pad) - pad, b = max(1024u * (lane + 1), pad) - pad;
-    const uint8_t* p = out + mem.ooff;
-    uint32_t c = 0;
-    uint32_t i = a;
-    for (; i < b && ((mem.ooff + i) & 3); ++i) c = T[(c ^ p[i]) & 0xFF] ^ (c >> 8);
-    for (; i + 4 <= b; i += 4) {
-        c ^= *(const uint32_t*)(p + i);
-        c = T[c & 0xFF] ^ (c >> 8);
-        c = T[c & 0xFF] ^ (c >> 8);
-        c = T[c & 0xFF] ^ (c >> 8);
-        c = T[c & 0xFF] ^ (c >> 8);
+    if (mem.isize == 0) {
+        if (lane == 0 && mem.crc != 0) {
+            status[m] = GZ_E_CRC;
+            atomicOr(any_error, 1u);
+        }
+        return;
     }
-    for (; i < b; ++i) c = T[(c ^ p[i]) & 0xFF] ^ (c >> 8);
-    // tree: raw(A || B) = raw(A) * x^(8|B|) ^ raw(B)
+    const uint32_t chunks = (mem.isize + 255) >> 8;
+    const uint64_t end = mem.ooff + mem.isize;
+    // dword q of chunk k starts at byte end - 256 (chunks - k) + 4 lane
+    const int64_t q0 = (int64_t)end - 256 * (int64_t)chunks + 4 * (int64_t)lane;
+    const uint32_t sh = (uint32_t)(end & 3);  // every q has the same misalignment
+    auto dword = [&](uint32_t k) -> uint32_t {
+        const int64_t q = q0 + 256 * (int64_t)k;
+        if (q + 4 <= (int64_t)mem.ooff) return 0u;  // wholly in the virtual front
+        const uint64_t w = (uint64_t)max(q, (int64_t)mem.ooff) & ~(uint64_t)3;  // never before the member's word
+        const uint64_t wq = (uint64_t)(q & ~(int64_t)3);
+        uint32_t lo = *(const uint32_t*)(out + w);
+        if (w != wq) lo = 0u;  // bytes before the member: masked below anyway
+        uint32_t d = lo;
+        if (sh) {
+            const uint32_t hi = *(const uint32_t*)(out + wq + 4);  // same aligned word as a valid byte
+            d = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        }
+        if (q < (int64_t)mem.ooff) d &= 0xFFFFFFFFu << (8u * (uint32_t)(mem.ooff - q));
+        return d;
+    };
+    uint32_t t = 0;
+    uint32_t k = 0;
+    // four chunks in flight per step
+    for (; k + 4 < chunks; k += 4) {
+        const uint32_t d0 = dword(k), d1 = dword(k + 1), d2 = dword(k + 2), d3 = dword(k + 3);
+#define ADV(d)                                                                                       \
+        {                                                                                            \
+            const uint32_t x = t ^ (d);                                                              \
+            t = A[0][x & 0xFF] ^ A[1][(x >> 8) & 0xFF] ^ A[2][(x >> 16) & 0xFF] ^ A[3][x >> 24];    \
+        }
+        ADV(d0) ADV(d1) ADV(d2) ADV(d3)
+    }
+    for (; k + 1 < chunks; ++k) ADV(dword(k))
+#undef ADV
+    uint32_t c = t ^ dword(chunks - 1);
+    // tree over consecutive dwords: node of 2^k lanes = 4 * 2^k bytes
 #pragma unroll
-    for (uint32_t k = 0; k < 6; ++k) {
-        const uint32_t step = 1u << k;
+    for (uint32_t lv = 0; lv < 6; ++lv) {
+        const uint32_t step = 1u << lv;
         const uint32_t right = __shfl_down(c, step);
-        if ((lane & (2 * step - 1)) == 0) c = multmodp(consts->slice[k], c) ^ right;
+        if ((lane & (2 * step - 1)) == 0) c = multmodp(consts->x2n[5 + lv], c) ^ right;
     }
     if (lane == 0) {
+        c = multmodp(consts->x2n[5], c);  // lane 0's state is aligned to its dword's start: 4 more bytes
         // standard CRC: pre-condition 0xFFFFFFFF shifted over the data, post-xor
         const uint32_t crc = c ^ multmodp(x2nmodp(*consts, mem.isize, 3), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         if (crc != mem.crc) {
@@ -775,7 +811,7 @@ hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint
 hipError_t launch_gz_crc(const uint8_t* out, const GzMember* members, uint32_t n, const GzCrcConsts* consts,
                          uint32_t* status, uint32_t* any_error, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gz_crc_kernel, dim3(n), dim3(64), 0, stream, out, members, n, consts, status, any_error);
+    hipLaunchKernelGGL(gz_crc_kernel, dim3((n + kCrcMembersPerBlock - 1) / kCrcMembersPerBlock), dim3(256), 0, stream, out, members, n, consts, status, any_error);
     return hipGetLastError();
 }
 

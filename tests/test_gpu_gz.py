@@ -99,6 +99,19 @@ def test_inflate_small_members_and_fixed_tables_after_dynamic(gpu_ctx):
     assert bgzf_inflate(gpu_ctx, member) == plain
 
 
+@pytest.mark.parametrize("block", [1, 3, 255, 256, 257, 4099])
+def test_inflate_member_sizes(gpu_ctx, block):
+    # every output misalignment and partial 256-byte CRC chunk; a 1-byte
+    # member at output offset 0 makes the CRC's virtual front reach before the buffer
+    data = fastq_text(40, 14)[: 3 * block + 7] if block > 3 else fastq_text(4, 14)[:601]
+    blob = bgzf_compress(data, 6, 0, block=block)
+    assert bgzf_inflate(gpu_ctx, blob) == data
+    bad = bytearray(blob)
+    bad[len(blob) - 28 - 8] ^= 0x80  # CRC of the last data member (the EOF block follows)
+    with pytest.raises(MswError, match="incorrect data check"):
+        bgzf_inflate(gpu_ctx, bytes(bad))
+
+
 def test_inflate_large_many_spans(gpu_ctx):
     data = fastq_text(60_000, 12) * 2  # ~40 MB: thousands of members in one launch
     blob = bgzf_compress(data, 6)
