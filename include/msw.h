@@ -220,6 +220,13 @@ int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* enqueued on `stream` (NULL = the context's compute stream); dst should be pinned */
 int msw_memcpy_d2h_async(msw_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
 int msw_synchronize(msw_ctx* ctx);
+/* A host-waitable point in `stream`'s work (NULL = the context's compute
+ * stream): msw_fence_wait blocks until everything enqueued on that stream
+ * before msw_fence_record has finished, without waiting for what came after
+ * (msw_synchronize drains all of the context's streams).  A fence is waited
+ * on once; the context keeps unwaited fences until it is destroyed. */
+int msw_fence_record(msw_ctx* ctx, void* stream, uint64_t* fence);
+int msw_fence_wait(msw_ctx* ctx, uint64_t fence);
 
 /* Counters of the host-batch calls (msw_align_batch*, msw_align_reads*) on a
  * context, for run records (the reference's BenchmarkResult,

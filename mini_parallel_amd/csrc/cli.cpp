@@ -530,8 +530,10 @@ struct WgsReport {
     int readers = 0;
     int host_threads = 0;
     std::vector<msw_stats_t> gpu;  // per worker: kernel time and algorithmic bytes (msw_ctx_stats)
+    std::vector<int> gpu_dev;      // device ordinal of each gpu[] entry (workers may share a GPU)
     bool gpu_inflate = false;      // lane files inflated and parsed on the GPUs
     double setup_ms = 0;           // worker setup before the clock started (contexts, genome, buffers)
+    double teardown_ms = 0;        // release after the last results, outside the clock
     unsigned long long gz_in = 0, gz_out = 0;  // compressed / inflated bytes (GPU lane reader)
 };
 
@@ -595,6 +597,22 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     const auto t_setup = Clock::now();
     auto t_all = t_setup;
     StartGate gate;
+    // the clock stops when the last worker has its last results on the host;
+    // teardown (reader / context / genome release) is reported apart, like setup
+    std::atomic<long long> t_done_ns{0};
+    auto mark_done = [&]() {
+        const long long t = Clock::now().time_since_epoch().count();
+        long long cur = t_done_ns.load();
+        while (t > cur && !t_done_ns.compare_exchange_weak(cur, t)) {
+        }
+    };
+    auto wall_and_teardown = [&](WgsReport& rep) {
+        const double total = ms_since(t_all);
+        const long long d = t_done_ns.load();
+        rep.wall_ms = d ? std::chrono::duration<double, std::milli>(Clock::time_point(Clock::duration(d)) - t_all).count()
+                        : total;
+        rep.teardown_ms = total - rep.wall_ms;
+    };
 
     auto finish_file = [&](size_t fi) {
         FileState& f = *st[fi];
@@ -654,6 +672,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     uint8_t* h = nullptr;  // pinned: score i32 | ei i16 | ej i16 | rlen u16 | wlen u16
                     uint64_t n = 0, first = 0;
                     size_t fi = 0;
+                    uint64_t fence = 0;  // after the batch's copy-back (msw_fence_record)
                     bool live = false;
                 } res[2];
                 const size_t rec = 4 + 2 + 2 + 2 + 2;
@@ -667,117 +686,155 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         die(std::string("GPU lane reader buffers: ") + msw_last_error());
                 }
                 unsigned long long alg_local = 0;
+                // per file this worker has open: batches in flight, reader done
+                std::map<size_t, std::pair<int, bool>> open_files;
+                auto maybe_finish = [&](size_t fi) {
+                    auto it = open_files.find(fi);
+                    if (it == open_files.end() || it->second.first > 0 || !it->second.second) return;
+                    open_files.erase(it);
+                    finish_file(fi);
+                };
                 // host side of a finished batch: sums, cells, per-read records
                 auto settle = [&](Res& r) {
                     if (!r.live) return;
                     r.live = false;
                     FileState& f = *st[r.fi];
-                    if (msw_synchronize(ctx.h) != MSW_OK) {
+                    if (msw_fence_wait(ctx.h, r.fence) != MSW_OK) {
                         fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
                         f.failed = true;
-                        return;
-                    }
-                    const int32_t* sc32 = (const int32_t*)r.h;
-                    const int16_t* ei = (const int16_t*)(r.h + batch * 4);
-                    const int16_t* ej = ei + batch;
-                    const uint16_t* rl = (const uint16_t*)(ej + batch);
-                    const uint16_t* wl = rl + batch;
-                    long long sum = 0;
-                    unsigned long long cl = 0, nb = 0, nw = 0;
-                    for (uint64_t i = 0; i < r.n; ++i) {
-                        sum += sc32[i];
-                        cl += (unsigned long long)rl[i] * wl[i];
-                        nb += rl[i];
-                        nw += wl[i];
-                    }
-                    alg_local += nb + nw + (sc.want_coords ? 8ull : 4ull) * r.n;
-                    f.score += sum;
-                    f.bases += nb;
-                    f.reads += r.n;
-                    cells += cl;
-                    if (f.scores_fd >= 0) {
-                        std::vector<uint8_t> out(r.n * 8);
+                    } else {
+                        const int32_t* sc32 = (const int32_t*)r.h;
+                        const int16_t* ei = (const int16_t*)(r.h + batch * 4);
+                        const int16_t* ej = ei + batch;
+                        const uint16_t* rl = (const uint16_t*)(ej + batch);
+                        const uint16_t* wl = rl + batch;
+                        long long sum = 0;
+                        unsigned long long cl = 0, nb = 0, nw = 0;
                         for (uint64_t i = 0; i < r.n; ++i) {
-                            memcpy(&out[i * 8], &sc32[i], 4);
-                            memcpy(&out[i * 8 + 4], &ei[i], 2);
-                            memcpy(&out[i * 8 + 6], &ej[i], 2);
+                            sum += sc32[i];
+                            cl += (unsigned long long)rl[i] * wl[i];
+                            nb += rl[i];
+                            nw += wl[i];
                         }
-                        if (pwrite(f.scores_fd, out.data(), out.size(), (off_t)(r.first * 8)) != (ssize_t)out.size()) {
-                            fprintf(stderr, "  error writing scores for %s\n", f.path.c_str());
-                            f.failed = true;
+                        alg_local += nb + nw + (sc.want_coords ? 8ull : 4ull) * r.n;
+                        f.score += sum;
+                        f.bases += nb;
+                        f.reads += r.n;
+                        cells += cl;
+                        if (f.scores_fd >= 0) {
+                            std::vector<uint8_t> out(r.n * 8);
+                            for (uint64_t i = 0; i < r.n; ++i) {
+                                memcpy(&out[i * 8], &sc32[i], 4);
+                                memcpy(&out[i * 8 + 4], &ei[i], 2);
+                                memcpy(&out[i * 8 + 6], &ej[i], 2);
+                            }
+                            if (pwrite(f.scores_fd, out.data(), out.size(), (off_t)(r.first * 8)) !=
+                                (ssize_t)out.size()) {
+                                fprintf(stderr, "  error writing scores for %s\n", f.path.c_str());
+                                f.failed = true;
+                            }
                         }
                     }
+                    open_files[r.fi].first -= 1;
+                    maybe_finish(r.fi);
                 };
                 int cur = 0;
                 msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
                 if (msw_gfastq_open(ctx.h, nullptr, kReadStride, batch, 1, 0, &gr) != MSW_OK)
                     die(std::string("GPU lane reader: ") + msw_last_error());
-                gate.arrive();
-                for (;;) {
-                    const size_t k = next_file.fetch_add(1);
-                    if (k >= todo.size()) break;
-                    const size_t fi = todo[k];
-                    FileState& f = *st[fi];
-                    f.t0 = Clock::now();
-                    if (!a.scores_out.empty()) {
-                        const size_t slash = f.path.find_last_of('/');
-                        const std::string out = a.scores_out + "/" +
-                                                (slash == std::string::npos ? f.path : f.path.substr(slash + 1)) +
-                                                ".scores";
-                        f.scores_fd = open(out.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
-                        if (f.scores_fd < 0) die("error: cannot create " + out);
-                    }
-                    printf("  Processing file %zu/%zu: %s (GPU inflate)\n", fi + 1, files.size(), f.path.c_str());
-                    fflush(stdout);
-                    const int orc = msw_gfastq_reset(gr, f.path.c_str());
-                    bool ok = orc == MSW_OK;
-                    if (!ok) {
-                        f.error = msw_last_error();
-                        fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
-                        f.failed = true;
-                    }
-                    while (ok) {
-                        msw_dev_reads_t d;
-                        if (msw_gfastq_next(gr, nullptr, &d) != MSW_OK) {
+                // the reader's stats of the file it just finished
+                auto reader_done = [&](size_t fi) {
+                    uint64_t bi = 0, bo = 0;
+                    msw_gfastq_stats(gr, nullptr, nullptr, nullptr, nullptr, &bi, &bo);
+                    gz_in += bi;
+                    gz_out += bo;
+                    st[fi]->reader_done = true;
+                    open_files[fi].second = true;
+                    maybe_finish(fi);
+                };
+                // next file for this worker: reset the reader (its compressed
+                // bytes start loading in the background), false when none is left
+                auto open_next = [&](size_t* fi_out) -> bool {
+                    for (;;) {
+                        const size_t k = next_file.fetch_add(1);
+                        if (k >= todo.size()) return false;
+                        const size_t fi = todo[k];
+                        FileState& f = *st[fi];
+                        f.t0 = Clock::now();
+                        open_files[fi] = {0, false};
+                        if (!a.scores_out.empty()) {
+                            const size_t slash = f.path.find_last_of('/');
+                            const std::string out = a.scores_out + "/" +
+                                                    (slash == std::string::npos ? f.path : f.path.substr(slash + 1)) +
+                                                    ".scores";
+                            f.scores_fd = open(out.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+                            if (f.scores_fd < 0) die("error: cannot create " + out);
+                        }
+                        printf("  Processing file %zu/%zu: %s (GPU inflate)\n", fi + 1, files.size(), f.path.c_str());
+                        fflush(stdout);
+                        if (msw_gfastq_reset(gr, f.path.c_str()) != MSW_OK) {
                             f.error = msw_last_error();
                             fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
                             f.failed = true;
-                            ok = false;
-                            break;
+                            reader_done(fi);
+                            continue;
                         }
-                        if (d.n == 0) break;
-                        Res& r = res[cur];
-                        settle(r);  // the batch before last used this result set
-                        msw_out_t o{r.d_score, r.d_ei, r.d_ej};
-                        if (msw_align_reads_device(ctx.h, &sc, gen, d.reads, d.read_len, d.read_stride, d.pos, d.n,
-                                                   a.window > 0 ? (uint32_t)a.window : 0u, d.max_len, &o, r.d_wlen,
-                                                   nullptr) != MSW_OK ||
-                            msw_memcpy_d2h_async(ctx.h, r.h, r.d_score, d.n * 4, nullptr) != MSW_OK ||
-                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 4, r.d_ei, d.n * 2, nullptr) != MSW_OK ||
-                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 6, r.d_ej, d.n * 2, nullptr) != MSW_OK ||
-                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 8, d.read_len, d.n * 2, nullptr) != MSW_OK ||
-                            msw_memcpy_d2h_async(ctx.h, r.h + batch * 10, r.d_wlen, d.n * 2, nullptr) != MSW_OK) {
-                            fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
-                            f.failed = true;
-                            break;
-                        }
-                        r.n = d.n;
-                        r.first = d.first_read;
-                        r.fi = fi;
-                        r.live = true;
-                        cur ^= 1;
+                        *fi_out = fi;
+                        return true;
                     }
-                    settle(res[cur ^ 1]);
-                    settle(res[cur]);
-                    if (gr) {
-                        uint64_t bi = 0, bo = 0;
-                        msw_gfastq_stats(gr, nullptr, nullptr, nullptr, nullptr, &bi, &bo);
-                        gz_in += bi;
-                        gz_out += bo;
+                };
+                gate.arrive();
+                // One loop over the batches of all of this worker's files: a
+                // file's last batches are settled after the next file's first
+                // batch is launched, so the next file's read, inflate and parse
+                // (reader stream) run beside this file's scoring (compute stream).
+                size_t fi = 0;
+                bool have = open_next(&fi);
+                while (have) {
+                    FileState& f = *st[fi];
+                    msw_dev_reads_t d;
+                    if (msw_gfastq_next(gr, nullptr, &d) != MSW_OK) {
+                        f.error = msw_last_error();
+                        fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
+                        f.failed = true;
+                        reader_done(fi);
+                        have = open_next(&fi);
+                        continue;
                     }
-                    f.reader_done = true;
-                    finish_file(fi);
+                    if (d.n == 0) {
+                        reader_done(fi);
+                        have = open_next(&fi);
+                        continue;
+                    }
+                    Res& r = res[cur];
+                    settle(r);  // the batch before last used this result set
+                    msw_out_t o{r.d_score, r.d_ei, r.d_ej};
+                    if (msw_align_reads_device(ctx.h, &sc, gen, d.reads, d.read_len, d.read_stride, d.pos, d.n,
+                                               a.window > 0 ? (uint32_t)a.window : 0u, d.max_len, &o, r.d_wlen,
+                                               nullptr) != MSW_OK ||
+                        msw_memcpy_d2h_async(ctx.h, r.h, r.d_score, d.n * 4, nullptr) != MSW_OK ||
+                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 4, r.d_ei, d.n * 2, nullptr) != MSW_OK ||
+                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 6, r.d_ej, d.n * 2, nullptr) != MSW_OK ||
+                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 8, d.read_len, d.n * 2, nullptr) != MSW_OK ||
+                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 10, r.d_wlen, d.n * 2, nullptr) != MSW_OK ||
+                        msw_fence_record(ctx.h, nullptr, &r.fence) != MSW_OK) {
+                        fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
+                        f.failed = true;
+                        (void)msw_synchronize(ctx.h);
+                        reader_done(fi);
+                        have = open_next(&fi);
+                        continue;
+                    }
+                    r.n = d.n;
+                    r.first = d.first_read;
+                    r.fi = fi;
+                    r.live = true;
+                    open_files[fi].first += 1;
+                    cur ^= 1;
                 }
+                settle(res[cur]);
+                settle(res[cur ^ 1]);
+                mark_done();
                 msw_gfastq_close(gr);
                 for (Res& r : res) {
                     msw_dev_free(ctx.h, r.d_score);
@@ -799,11 +856,12 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         rep.setup_ms = std::chrono::duration<double, std::milli>(t_all - t_setup).count();
         rep.gz_in = gz_in.load();
         rep.gz_out = gz_out.load();
-        rep.wall_ms = ms_since(t_all);
+        wall_and_teardown(rep);
         rep.cells = cells.load();
         rep.readers = 0;
         rep.host_threads = nworkers;
         rep.gpu = gstats;
+        for (int wi = 0; wi < nworkers; ++wi) rep.gpu_dev.push_back(devices[wi % ngpu].ordinal);
         rep.gpu_inflate = true;
         for (size_t i = 0; i < files.size(); ++i)
             if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
@@ -1024,6 +1082,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 settle(*pending.front());
                 pending.pop_front();
             }
+            mark_done();
             msw_genome_destroy(gen);
             msw_ctx_stats(ctx.h, &gstats[(size_t)g], 0);
         });
@@ -1035,11 +1094,12 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     for (size_t fi : todo) finish_file(fi);  // no-op for files already finished
     WgsReport rep;
     rep.setup_ms = std::chrono::duration<double, std::milli>(t_all - t_setup).count();
-    rep.wall_ms = ms_since(t_all);
+    wall_and_teardown(rep);
     rep.cells = cells.load();
     rep.readers = nreaders;
     rep.host_threads = host_threads;
     rep.gpu = gstats;
+    for (const Device& d : devices) rep.gpu_dev.push_back(d.ordinal);
     for (size_t i = 0; i < files.size(); ++i)
         if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
     return rep;
@@ -1119,7 +1179,6 @@ int main(int argc, char** argv) {
         // Run record: the reference's BenchmarkResult fields (tools/benchmark.rs:17-34;
         // its fake gpu_utilization_avg / gpu_memory_used_mb are dropped) plus GCUPS
         // (kernel and end to end), HBM GB/s and roofline fractions.
-        const int ng = (int)workers.size();
         const double secs = std::max(rep.wall_ms / 1000.0, 1e-9);
         char ts[64];
         {
@@ -1137,14 +1196,18 @@ int main(int argc, char** argv) {
         }
         const double gcups_e2e = rep.cells ? rep.cells / (rep.wall_ms * 1e6) : 0.0;
         // Kernel rate: the job's cells over the busiest GPU's kernel time
-        // (HIP events around every chunk's scoring launch, msw_ctx_stats).
+        // (HIP events around every chunk's scoring launch, msw_ctx_stats),
+        // the kernel time of the workers sharing a GPU summed.
         double kmax = 0, ksum = 0;
         unsigned long long alg = 0;
-        for (const msw_stats_t& g : rep.gpu) {
-            kmax = std::max(kmax, g.kernel_ms);
-            ksum += g.kernel_ms;
-            alg += g.alg_bytes;
+        std::map<int, double> per_dev;
+        for (size_t i = 0; i < rep.gpu.size(); ++i) {
+            per_dev[i < rep.gpu_dev.size() ? rep.gpu_dev[i] : (int)i] += rep.gpu[i].kernel_ms;
+            ksum += rep.gpu[i].kernel_ms;
+            alg += rep.gpu[i].alg_bytes;
         }
+        for (const auto& kv : per_dev) kmax = std::max(kmax, kv.second);
+        const int ng = (int)per_dev.size();  // physical GPUs
         const bool sw_mode = a.score_mode == "sw";
         const double gcups = kmax > 0 && sw_mode ? rep.cells / (kmax * 1e6) : 0.0;
         const double hbm_gbps = kmax > 0 ? alg / (kmax * 1e6) : 0.0;
@@ -1166,13 +1229,13 @@ int main(int argc, char** argv) {
           << ", \"system_info\": {\"gpu_name\": \"" << json_escape(devices.empty() ? "" : devices[0].name)
           << "\", \"gpu_memory_gb\": " << (devices.empty() ? 0.0 : devices[0].memory_gb)
           << ", \"cpu_cores\": " << std::thread::hardware_concurrency() << ", \"total_ram_gb\": " << ram_gb << "}"
-          << ", \"num_gpus\": " << ng << ", \"host_cores\": " << std::thread::hardware_concurrency()
+          << ", \"num_gpus\": " << workers.size() << ", \"physical_gpus\": " << ng << ", \"host_cores\": " << std::thread::hardware_concurrency()
           << ", \"host_cpus_usable\": " << usable_cpus() << ", \"host_threads\": " << rep.host_threads
           << ", \"cells\": " << rep.cells << ", \"gcups\": " << gcups << ", \"gcups_end_to_end\": " << gcups_e2e
           << ", \"kernel_ms\": " << kmax << ", \"gpu_busy_fraction\": " << busy
           << ", \"alg_bytes\": " << alg << ", \"hbm_gbps\": " << hbm_gbps
           << ", \"roofline_fraction_hbm\": " << frac_hbm << ", \"roofline_fraction_valu\": " << frac_valu
-          << ", \"gpu_inflate\": " << (rep.gpu_inflate ? "true" : "false") << ", \"setup_ms\": " << rep.setup_ms
+          << ", \"gpu_inflate\": " << (rep.gpu_inflate ? "true" : "false") << ", \"setup_ms\": " << rep.setup_ms << ", \"teardown_ms\": " << rep.teardown_ms
           << ", \"inflate_bytes_in\": " << rep.gz_in << ", \"inflate_bytes_out\": " << rep.gz_out
           << ", \"reads_per_second\": " << reads / secs << "}\n";
         write_json(a.json, j.str());

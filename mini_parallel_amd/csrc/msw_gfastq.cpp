@@ -259,8 +259,13 @@ struct msw_gfastq {
     int device = 0;
     hipStream_t rs = nullptr;          // the reader's own stream (inflate + parse)
     hipEvent_t parsed = nullptr;       // phase B of the current span done
-    hipEvent_t emitted = nullptr;      // the last emit (on the caller's stream)
-    bool emitted_valid = false;
+    // per span buffer i (dout[i] and its line arrays pb[i]): the last emit
+    // that read it, on the caller's stream.  A span only waits for the emits
+    // of the span two before it, so inflating and parsing the next span (or
+    // the next file) runs beside the current span's emits and scoring.
+    hipEvent_t emitted[2] = {nullptr, nullptr};
+    bool emitted_valid[2] = {false, false};
+    int last_buf = 1;                  // buffer of the latest span (any file); the next takes the other
     FILE* f = nullptr;
     std::string path;
     uint64_t fsize = 0, fread_off = 0;
@@ -281,16 +286,21 @@ struct msw_gfastq {
     Inflater inf;
     std::vector<msw::GzMember> mem;
 
-    // span buffers: [kCarry | span + kPad]; cur = the parsed one
+    // span buffers: [kCarry | span + kPad]; cur = the parsed one (-1: none yet in this file)
     uint8_t* dout[2] = {nullptr, nullptr};
     int cur = -1;
     uint64_t cur_off = 0, cur_len = 0, tail_start = 0;  // parse window [cur_off, cur_off + cur_len) of dout[cur]
     bool started = false, at_eof = false;
 
-    // parse arrays
-    msw::ParseBufs pb{};
-    size_t tile_cap = 0, tile_hi_cap = 0, line_cap = 0, vidx_cap = 0, v_cap = 0, blk_cap = 0;
+    // parse arrays: tile counts shared (only the reader stream uses them), line
+    // arrays per span buffer (the emits read them)
+    uint32_t* tile_nl = nullptr;
+    uint32_t* tile_hi = nullptr;
+    size_t tile_cap = 0, tile_hi_cap = 0;
+    msw::ParseBufs pb[2]{};
+    size_t line_cap[2] = {0, 0}, vidx_cap[2] = {0, 0}, v_cap[2] = {0, 0}, blk_cap[2] = {0, 0};
     msw::ParseState* d_state = nullptr;
+    msw::ParseState* d_state0 = nullptr;  // a file's initial state (copied on the reader stream)
     msw::ParseOut* d_out = nullptr;
     msw::ParseOut* h_out = nullptr;  // pinned
     msw::ParseState* h_state = nullptr;  // pinned
@@ -327,20 +337,24 @@ void release(msw_gfastq* g) {
         if (g->s_rlen[i]) (void)hipFree(g->s_rlen[i]);
         if (g->s_pos[i]) (void)hipFree(g->s_pos[i]);
     }
-    if (g->pb.tile_nl) (void)hipFree(g->pb.tile_nl);
-    if (g->pb.tile_hi) (void)hipFree(g->pb.tile_hi);
-    if (g->pb.line_end) (void)hipFree(g->pb.line_end);
-    if (g->pb.vidx) (void)hipFree(g->pb.vidx);
-    if (g->pb.vline) (void)hipFree(g->pb.vline);
-    if (g->pb.blk) (void)hipFree(g->pb.blk);
+    if (g->tile_nl) (void)hipFree(g->tile_nl);
+    if (g->tile_hi) (void)hipFree(g->tile_hi);
+    for (msw::ParseBufs& b : g->pb) {
+        if (b.line_end) (void)hipFree(b.line_end);
+        if (b.vidx) (void)hipFree(b.vidx);
+        if (b.vline) (void)hipFree(b.vline);
+        if (b.blk) (void)hipFree(b.blk);
+    }
     if (g->d_state) (void)hipFree(g->d_state);
+    if (g->d_state0) (void)hipFree(g->d_state0);
     if (g->d_out) (void)hipFree(g->d_out);
     if (g->h_out) (void)hipHostFree(g->h_out);
     if (g->h_state) (void)hipHostFree(g->h_state);
     if (g->hc) (void)hipHostFree(g->hc);
     g->inf.release();
     if (g->parsed) (void)hipEventDestroy(g->parsed);
-    if (g->emitted) (void)hipEventDestroy(g->emitted);
+    for (hipEvent_t e : g->emitted)
+        if (e) (void)hipEventDestroy(e);
     if (g->rs) (void)hipStreamDestroy(g->rs);
     delete g;
 }
@@ -364,12 +378,13 @@ int fill_compressed(msw_gfastq* g, size_t want) {
 // at_eof set when the file has no more data.
 int fill_compressed(msw_gfastq* g, size_t want);
 
-// Start reading ahead ~one span's compressed bytes (the last span's size) in
-// the background; next_span joins before it touches hc.
+// Start reading ahead ~one span's compressed bytes (the last span's size; a
+// whole staging buffer at the start of a file) in the background; next_span
+// joins before it touches hc.
 void start_filler(msw_gfastq* g) {
     join_filler(g);
     if (g->fread_off >= g->fsize || g->hc_len >= g->hc_cap) return;
-    const size_t want = std::min(g->hc_cap, g->hc_len + g->last_used + kReadPiece);
+    const size_t want = g->cur < 0 ? g->hc_cap : std::min(g->hc_cap, g->hc_len + g->last_used + kReadPiece);
     g->fill_rc = 0;
     g->filler = std::thread([g, want]() {
         g->fill_rc = fill_compressed(g, want);
@@ -385,7 +400,7 @@ int next_span(msw_gfastq* g) {
     int rc;
     static const bool trace = getenv("MSW_GFASTQ_TRACE") != nullptr;
     const double t0 = trace ? now_ms() : 0.0;
-    const int nx = g->cur < 0 ? 0 : 1 - g->cur;
+    const int nx = 1 - g->last_buf;
     join_filler(g);
     if (g->fill_rc) return set_error(g->fill_rc, "%s", g->fill_msg.c_str());
     // 1. whole members whose output fits the span (compressed <= span bytes + 1 MiB)
@@ -410,8 +425,10 @@ int next_span(msw_gfastq* g) {
 
     const double t_read = trace ? now_ms() : 0.0;
     hipStream_t s = g->rs;
-    // the buffer we write and the parse arrays are read by the previous span's emits
-    if (g->emitted_valid) GZ_TRY(hipStreamWaitEvent(s, g->emitted, 0));
+    // dout[nx] and its line arrays were last read by the emits of the span
+    // before the current one (long finished, normally); the current span's
+    // emits and the caller's scoring keep running
+    if (g->emitted_valid[nx]) GZ_TRY(hipStreamWaitEvent(s, g->emitted[nx], 0));
     // 2. inflate + CRC into dout[nx] at kCarry
     if ((rc = g->inf.run(g->hc, used, g->mem, g->dout[nx], s))) return rc;
     // 3. the previous span's unfinished line goes right in front
@@ -423,7 +440,7 @@ int next_span(msw_gfastq* g) {
         GZ_TRY(hipMemcpyAsync(g->dout[nx] + kCarry - carry, g->dout[g->cur] + g->cur_off + g->tail_start, carry,
                               hipMemcpyDeviceToDevice, s));
     // 4. parse phase A over [kCarry - carry, kCarry + obytes), from a 16-byte aligned base
-    msw::ParseBufs& b = g->pb;
+    msw::ParseBufs& b = g->pb[nx];
     const uint64_t base = (kCarry - carry) & ~(uint64_t)15;
     b.buf = g->dout[nx] + base;
     b.begin = (uint32_t)(kCarry - carry - base);
@@ -431,8 +448,10 @@ int next_span(msw_gfastq* g) {
     b.eof = last ? 1u : 0u;
     b.want_pos = g->want_pos ? 1u : 0u;
     b.ntiles = (uint32_t)((b.len + msw::kParseTile - 1) / msw::kParseTile);
-    if ((rc = grow(&b.tile_nl, &g->tile_cap, (size_t)b.ntiles + 1))) return rc;
-    if ((rc = grow(&b.tile_hi, &g->tile_hi_cap, (size_t)b.ntiles + 1))) return rc;
+    if ((rc = grow(&g->tile_nl, &g->tile_cap, (size_t)b.ntiles + 1))) return rc;
+    if ((rc = grow(&g->tile_hi, &g->tile_hi_cap, (size_t)b.ntiles + 1))) return rc;
+    b.tile_nl = g->tile_nl;
+    b.tile_hi = g->tile_hi;
     b.line_cap = ~0ull;
     b.state = g->d_state;
     b.out = g->d_out;
@@ -452,12 +471,12 @@ int next_span(msw_gfastq* g) {
     const uint64_t nlines = g->h_out->lines;
     const bool any_high = g->h_out->any_high != 0;
     // 5. size the line arrays, phase B
-    if ((rc = grow(&b.line_end, &g->line_cap, (size_t)nlines + 1))) return rc;
-    b.line_cap = g->line_cap;
+    if ((rc = grow(&b.line_end, &g->line_cap[nx], (size_t)nlines + 1))) return rc;
+    b.line_cap = g->line_cap[nx];
     if (any_high) {
-        if ((rc = grow(&b.vidx, &g->vidx_cap, (size_t)nlines + 1))) return rc;
-        if ((rc = grow(&b.vline, &g->v_cap, (size_t)nlines + 1))) return rc;
-        if ((rc = grow(&b.blk, &g->blk_cap, (size_t)(nlines / 1024 + 2)))) return rc;
+        if ((rc = grow(&b.vidx, &g->vidx_cap[nx], (size_t)nlines + 1))) return rc;
+        if ((rc = grow(&b.vline, &g->v_cap[nx], (size_t)nlines + 1))) return rc;
+        if ((rc = grow(&b.blk, &g->blk_cap[nx], (size_t)(nlines / 1024 + 2)))) return rc;
     }
     GZ_TRY(msw::launch_parse_b(b, nlines, any_high, s));
     GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
@@ -478,6 +497,7 @@ int next_span(msw_gfastq* g) {
     g->bytes_in += used;
     g->bytes_out += obytes;
     g->cur = nx;
+    g->last_buf = nx;
     g->cur_off = base;
     g->cur_len = b.len;
     g->tail_start = o.tail_start;
@@ -529,13 +549,12 @@ int open_file(msw_gfastq* g, const char* path) {
         return set_error(MSW_E_INVALID, "%s is not a BGZF file", path);
     }
     if (g->d_state) {
+        // back to line 0, in order on the reader stream (the emits never read
+        // the state); the previous file's batches stay valid on the caller's stream
         GZ_TRY(hipSetDevice(g->device));
-        if (g->emitted_valid) GZ_TRY(hipStreamWaitEvent(g->rs, g->emitted, 0));
-        const msw::ParseState st0{0, 0, -1, 0};
-        *g->h_state = st0;
-        GZ_TRY(hipMemcpyAsync(g->d_state, g->h_state, sizeof(st0), hipMemcpyHostToDevice, g->rs));
-        GZ_TRY(hipStreamSynchronize(g->rs));
+        GZ_TRY(hipMemcpyAsync(g->d_state, g->d_state0, sizeof(msw::ParseState), hipMemcpyDeviceToDevice, g->rs));
     }
+    start_filler(g);  // the first span's compressed bytes, read while the caller finishes the last file
     return MSW_OK;
 }
 
@@ -581,7 +600,8 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     if ((rc = g->inf.init())) return bail(rc);
     if (hipStreamCreateWithFlags(&g->rs, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&g->parsed, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&g->emitted, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&g->emitted[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->emitted[1], hipEventDisableTiming) != hipSuccess)
         return bail(set_error(MSW_E_DEVICE, "stream/event creation failed"));
     // compressed staging: half a span (FASTQ compresses ~3-4x; less
     // compressible data just makes shorter spans) + room for one fread piece
@@ -599,9 +619,13 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
                                   (unsigned long long)(g->span >> 20)));
     }
     if (hipMalloc((void**)&g->d_state, sizeof(msw::ParseState)) != hipSuccess ||
+        hipMalloc((void**)&g->d_state0, sizeof(msw::ParseState)) != hipSuccess ||
         hipMalloc((void**)&g->d_out, sizeof(msw::ParseOut)) != hipSuccess ||
         hipHostMalloc((void**)&g->h_state, sizeof(msw::ParseState), hipHostMallocDefault) != hipSuccess)
         return bail(set_error(MSW_E_NOMEM, "hipMalloc failed (GPU lane reader state)"));
+    *g->h_state = msw::ParseState{0, 0, -1, 0};
+    if (hipMemcpy(g->d_state0, g->h_state, sizeof(msw::ParseState), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(set_error(MSW_E_DEVICE, "hipMemcpy failed (GPU lane reader state)"));
     if (path && (rc = open_file(g, path))) return bail(rc);
     if (!path) g->failed = MSW_E_INVALID;  // buffers only: msw_gfastq_reset names the first file
     *out = g;
@@ -640,10 +664,10 @@ int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {
     const int k = g->slot;
     g->slot ^= 1;
     GZ_TRY(hipStreamWaitEvent(cs, g->parsed, 0));
-    GZ_TRY(msw::launch_emit_reads(g->pb, g->sp, g->span_done, n, g->s_reads[k], g->s_rlen[k],
+    GZ_TRY(msw::launch_emit_reads(g->pb[g->cur], g->sp, g->span_done, n, g->s_reads[k], g->s_rlen[k],
                                   g->want_pos ? g->s_pos[k] : nullptr, cs));
-    GZ_TRY(hipEventRecord(g->emitted, cs));
-    g->emitted_valid = true;
+    GZ_TRY(hipEventRecord(g->emitted[g->cur], cs));
+    g->emitted_valid[g->cur] = true;
     out->reads = g->s_reads[k];
     out->read_len = g->s_rlen[k];
     out->pos = g->want_pos ? g->s_pos[k] : nullptr;

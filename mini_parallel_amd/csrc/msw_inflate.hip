@@ -795,8 +795,14 @@ hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint
         const char* e = getenv("MSW_GZ_RING_KB");
         return e ? atoi(e) : kDefaultRingKb;
     }();
-#define GZ_LAUNCH(R) hipLaunchKernelGGL(gz_inflate_kernel<R>, dim3(n), dim3(64), 0, stream, cdata, members, n, out, \
-                                         status, any_error, prof)
+    // MSW_GZ_LDS_PAD: extra (dynamic) LDS bytes per wave, which caps the
+    // inflate waves per CU and leaves registers for kernels sharing the GPU
+    static const uint32_t lds_pad = [] {
+        const char* e = getenv("MSW_GZ_LDS_PAD");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+#define GZ_LAUNCH(R) hipLaunchKernelGGL(gz_inflate_kernel<R>, dim3(n), dim3(64), lds_pad, stream, cdata, members, n, \
+                                         out, status, any_error, prof)
     switch (ring_kb) {
         case 2: GZ_LAUNCH(2048); break;
         case 4: GZ_LAUNCH(4096); break;

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <deque>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/msw.h"
@@ -233,6 +234,8 @@ struct msw_ctx {
     };
     std::deque<DevTiming> dev_timings;
     std::vector<hipEvent_t> free_events;
+    std::unordered_map<uint64_t, hipEvent_t> fences;  // msw_fence_record, not yet waited on
+    uint64_t next_fence = 1;
 };
 
 struct msw_genome {
@@ -988,6 +991,7 @@ void msw_ctx_destroy(msw_ctx* ctx) {
         (void)hipEventDestroy(t.k1);
     }
     for (hipEvent_t e : ctx->free_events) (void)hipEventDestroy(e);
+    for (auto& kv : ctx->fences) (void)hipEventDestroy(kv.second);
     if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
@@ -1450,6 +1454,35 @@ int msw_ctx_stats(msw_ctx* ctx, msw_stats_t* out, int reset) {
     if (set_device(ctx) == MSW_OK) harvest_dev_timings(ctx, true);
     *out = ctx->stats;
     if (reset) ctx->stats = msw_stats_t{};
+    return MSW_OK;
+}
+
+int msw_fence_record(msw_ctx* ctx, void* stream, uint64_t* fence) {
+    if (!ctx || !fence) return fail(MSW_E_INVALID, "ctx/fence is NULL");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    hipEvent_t e = take_event(ctx);
+    if (!e) return fail(MSW_E_DEVICE, "hipEventCreate failed");
+    if (hipEventRecord(e, stream ? (hipStream_t)stream : ctx->compute) != hipSuccess) {
+        ctx->free_events.push_back(e);
+        return fail(MSW_E_DEVICE, "hipEventRecord failed");
+    }
+    *fence = ctx->next_fence++;
+    ctx->fences.emplace(*fence, e);
+    return MSW_OK;
+}
+
+int msw_fence_wait(msw_ctx* ctx, uint64_t fence) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    auto it = ctx->fences.find(fence);
+    if (it == ctx->fences.end()) return fail(MSW_E_INVALID, "unknown fence %llu", (unsigned long long)fence);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    hipEvent_t e = it->second;
+    ctx->fences.erase(it);
+    const hipError_t err = hipEventSynchronize(e);
+    ctx->free_events.push_back(e);
+    if (err != hipSuccess) return fail(MSW_E_DEVICE, "GPU error before the fence: %s", hipGetErrorString(err));
     return MSW_OK;
 }
 

@@ -207,6 +207,8 @@ def test_full_wgs_config4_shape_two_workers(tmp_path, oracle, gpu_inflate):
         assert k in rec, k
     assert rec["gcups"] >= rec["gcups_end_to_end"] > 0
     assert 0 < rec["roofline_fraction_hbm"] < 1 and 0 < rec["roofline_fraction_valu"] < 1
+    # both workers share GPU 0: their kernel time adds up on one device
+    assert rec["physical_gpus"] == 1 and 0 < rec["gpu_busy_fraction"] <= 1
     assert rec["hbm_gbps"] > 0 and rec["cells"] == sum(int((b.read_len.astype(np.int64) * 300).sum())
                                                        for b in ds["batches"])
     ck = json.load(open(tmp_path / "checkpoint_c4.json"))
