@@ -93,8 +93,10 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
 int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out);
 /* Point an open reader at another lane file (same context, stride, batch
  * size and span): the device and pinned buffers are kept, so a worker that
- * walks many files allocates once.  Batches of the previous file must not be
- * used after the first msw_gfastq_next on the new one returns. */
+ * walks many files allocates once, and the new file's compressed bytes start
+ * loading in the background.  Batches keep the rule above across files (the
+ * two slabs alternate), so scoring enqueued on the previous file's last
+ * batches may still be running while the new file is inflated and parsed. */
 int msw_gfastq_reset(msw_gfastq* g, const char* path);
 /* lines (valid), reads, errors (invalid lines), bases, compressed and inflated bytes so far (this file) */
 void msw_gfastq_stats(const msw_gfastq* g, uint64_t* lines, uint64_t* reads, uint64_t* errors, uint64_t* bases,
