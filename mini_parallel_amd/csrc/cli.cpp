@@ -186,14 +186,17 @@ Args parse_args(int argc, char** argv) {
     return a;
 }
 
-msw_scoring_t scoring_of(const Args& a) {
+// Best cells cost ~1.5x the score-only kernel; --full-wgs needs them only for
+// --scores-out records (the per-file results are score sums), pair mode prints
+// them.
+msw_scoring_t scoring_of(const Args& a, bool want_coords) {
     msw_scoring_t sc;
     sc.match = a.match;
     sc.mismatch = a.mismatch;
     sc.gap_open = a.gap_model == "affine" ? a.gap_open : 0;
     sc.gap_extend = a.gap_extend;
     sc.affine = a.gap_model == "affine";
-    sc.want_coords = 1;
+    sc.want_coords = want_coords ? 1 : 0;
     return sc;
 }
 
@@ -660,7 +663,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
             workers.emplace_back([&, wi]() {
                 const int gi = wi % ngpu;
                 Ctx ctx(devices[gi].ordinal);
-                const msw_scoring_t sc = scoring_of(a);
+                const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
                 msw_genome* gen = nullptr;
                 if (msw_genome_create(ctx.h, (const uint8_t*)genome.data(), genome.size(), &gen) != MSW_OK)
                     die(std::string("GPU genome upload error: ") + msw_last_error());
@@ -966,7 +969,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     for (int g = 0; g < ngpu; ++g) {
         workers.emplace_back([&, g]() {
             Ctx ctx(devices[g].ordinal);
-            const msw_scoring_t sc = scoring_of(a);
+            const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
             // sw mode: the reference genome lives in this GPU's HBM; a chunk
             // ships reads + window positions, windows are cut on the GPU.
             msw_genome* gen = nullptr;
@@ -1211,10 +1214,13 @@ int main(int argc, char** argv) {
         const bool sw_mode = a.score_mode == "sw";
         const double gcups = kmax > 0 && sw_mode ? rep.cells / (kmax * 1e6) : 0.0;
         const double hbm_gbps = kmax > 0 ? alg / (kmax * 1e6) : 0.0;
-        // Per-GPU ceilings: 8 TB/s HBM; VALU issue of the best-cell loops
-        // (128 cells per 30.28 / 46.99 cycles per packed row-step x 1024 SIMDs x
-        // 2.4 GHz; bench.py CYCLES_PER_ROW_STEP).
-        const double valu_ceiling = a.gap_model == "affine" ? 6694.5 : 10389.5;
+        // Per-GPU ceilings: 8 TB/s HBM; VALU issue of the loop that ran (128
+        // cells per 19.16 / 30.28 / 35.88 / 46.99 cycles per packed row-step for
+        // linear / +coords / affine / +coords, x 1024 SIMDs x 2.4 GHz; bench.py
+        // CYCLES_PER_ROW_STEP).
+        const bool coords = !a.scores_out.empty();
+        const double valu_ceiling = a.gap_model == "affine" ? (coords ? 6694.5 : 8767.6)
+                                                            : (coords ? 10389.5 : 16418.2);
         const double frac_hbm = ng ? hbm_gbps / (8000.0 * ng) : 0.0;
         const double frac_valu = ng && sw_mode ? gcups / (valu_ceiling * ng) : 0.0;
         const double busy = ng && rep.wall_ms > 0 ? ksum / (ng * rep.wall_ms) : 0.0;
@@ -1304,7 +1310,7 @@ int main(int argc, char** argv) {
     }
 
     if (a.score_mode == "sw") {
-        msw_scoring_t sc = scoring_of(a);
+        msw_scoring_t sc = scoring_of(a, true);
         const size_t rs = std::max<size_t>(16, (a.seq1.size() + 15) / 16 * 16);
         const size_t ws = std::max<size_t>(16, (a.seq2.size() + 15) / 16 * 16);
         std::vector<uint8_t> r(rs, 0), w(ws, 0);
