@@ -1316,9 +1316,9 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> r(rs, 0), w(ws, 0);
         memcpy(r.data(), a.seq1.data(), a.seq1.size());
         memcpy(w.data(), a.seq2.data(), a.seq2.size());
-        if (a.seq1.size() > 0xFFFF || a.seq2.size() > 0xFFFF) {
+        if (a.seq1.size() > 32767 || a.seq2.size() > 32767) {
             fprintf(stderr, "GPU alignment error: sequence of %zu / %zu bases exceeds the kernel limits "
-                            "(read <= 256, window <= 4096)\n", a.seq1.size(), a.seq2.size());
+                            "(read <= 32767, window <= 32767)\n", a.seq1.size(), a.seq2.size());
             return 1;
         }
         uint16_t rl = (uint16_t)a.seq1.size(), wl = (uint16_t)a.seq2.size();

@@ -17,7 +17,12 @@ constexpr int kGroupLanes = 16;        // one DPP row
 constexpr int kPairsPerWave = 8;       // 4 groups x 2 packed pairs
 constexpr int kMaxReadLen = 256;       // KR <= 16
 constexpr int kMaxWinLen = 4096;
-constexpr int kLead = 32;              // sentinel words in front of each window stream
+constexpr int kLead = 32;
+// Pairs with a read > kMaxReadLen or a window > kMaxWinLen go to the long-pair
+// kernel (msw_long.hip): i32 cells, any length up to kMaxLongLen (the i16
+// best-cell coordinates of msw_out_t).
+constexpr int kMaxLongLen = 32767;
+constexpr int kLongMaxR = 8;           // rows per lane; strips of 64 * R rows              // sentinel words in front of each window stream
 
 // u32 words per lane-group stream: kLead + (max_win + 31) steps rounded to even
 // + 4 lookahead,
@@ -67,6 +72,10 @@ struct SwParams {
     // out_slot_base + slot): planned batches read them contiguously instead of
     // gathering two 2-byte lengths per pair through the order array.
     const uint32_t* slot_lens;
+    // Long pairs (sw_long_kernel, msw_long.hip): per-block boundary rows,
+    // long_cols i32 columns each (x2 for affine: H then F).
+    int32_t* long_scratch;
+    uint32_t long_cols;
 };
 
 // f16 bits of the cell value v * 2^-11 (|v| < 2048: exact, normal or zero).
@@ -134,8 +143,8 @@ hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, 
 constexpr uint32_t kGenomePad = 64;
 hipError_t launch_cut_windows(const uint8_t* genome, uint64_t glen, const int64_t* pos, const uint16_t* want,
                               uint8_t* out, uint16_t* out_len, uint32_t ws, uint64_t n, hipStream_t stream);
-// Same, for device-resident reads: want = window, or 2 x rlen[p] when window
-// is 0, capped at kMaxWinLen (msw_align_reads_device).
+// Same, for device-resident reads: want = window, or 2 x rlen[p] capped at
+// kMaxWinLen when window is 0 (msw_align_reads_device).
 hipError_t launch_cut_windows_for_reads(const uint8_t* genome, uint64_t glen, const int64_t* pos,
                                         const uint16_t* rlen, uint32_t window, uint8_t* out, uint16_t* out_len,
                                         uint32_t ws, uint64_t n, hipStream_t stream);
@@ -146,6 +155,17 @@ hipError_t launch_cut_windows_for_reads(const uint8_t* genome, uint64_t glen, co
 hipError_t launch_gather_results(const uint32_t* inv, const int32_t* src_score, const int16_t* src_i,
                                  const int16_t* src_j, int32_t* score, int16_t* end_i, int16_t* end_j, uint64_t n,
                                  hipStream_t stream);
+
+// Long pairs: R = rows per lane for a read-length bound (one strip of 64 * R
+// rows when it fits, else strips of 512); scratch columns per block; LDS bytes.
+int long_rows_per_lane(uint32_t max_read_len);
+uint32_t long_scratch_cols(uint32_t max_win_len);
+size_t long_lds_bytes(uint32_t max_win_len);
+// One wave per pair, `blocks` blocks striding over p.n_slots (order / slot
+// results as in launch_sw).  p.long_scratch must hold blocks x long_cols
+// (x2 affine) i32 when the read bound exceeds 64 * R rows.
+hipError_t launch_sw_long(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, uint32_t max_win_len,
+                          uint32_t blocks, hipStream_t stream);
 
 // smith_waterman_align restated: result must be zeroed before the launch.
 hipError_t launch_compat(const uint8_t* s1, const uint8_t* s2, int32_t* result, uint64_t L,

@@ -63,8 +63,8 @@ __global__ __launch_bounds__(256) void cut_windows_kernel(const uint8_t* __restr
     const uint32_t c = (uint32_t)(t - p * chunks);
     const uint64_t start = (uint64_t)pos[p];  // negative positions wrap past glen
     const uint64_t room = start < glen ? glen - start : 0;
-    // requested length: want[p], or (device-resident reads) --window / 2 x read length
-    const uint64_t wl = want ? want[p] : min(window ? window : 2u * rlen[p], (uint32_t)kMaxWinLen);
+    // requested length: want[p], or (device-resident reads) --window / 2 x read length (capped)
+    const uint64_t wl = want ? want[p] : (window ? window : min(2u * rlen[p], (uint32_t)kMaxWinLen));
     const int len = (int)min(min(wl, room), ws);
     if (out_len && c == 0) out_len[p] = (uint16_t)len;
     const int rem = len - 16 * (int)c;

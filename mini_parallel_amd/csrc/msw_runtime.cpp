@@ -123,17 +123,43 @@ bool f16_fits(const Scheme& s, uint32_t max_m, uint32_t max_n) {
     return s.f16_scheme && (uint64_t)s.match * (std::min(max_m, max_n) + 2u) < 2048u;
 }
 
-// Score bound: every cell value (and H + match) must stay a finite,
-// non-negative f16 bit pattern (< 0x7C00) for v_pk_maximum3_f16.
+// Length limits: pairs up to kMaxReadLen x kMaxWinLen run on the packed
+// 16-bit kernels (every cell value, <= match * (257 + 1) + bias < 0x7C00, is
+// a finite non-negative f16 bit pattern for v_pk_maximum3_f16); longer reads
+// or windows, up to kMaxLongLen (the i16 coordinates), on the i32 long-pair
+// kernel (msw_long.hip).
 int check_bounds(const Scheme& s, uint32_t max_m, uint32_t max_n) {
-    if (max_m > (uint32_t)msw::kMaxReadLen)
-        return fail(MSW_E_RANGE, "read length %u > %d", max_m, msw::kMaxReadLen);
-    if (max_n > (uint32_t)msw::kMaxWinLen)
-        return fail(MSW_E_RANGE, "window length %u > %d", max_n, msw::kMaxWinLen);
-    const uint64_t bound = (uint64_t)s.match * (std::min(max_m, max_n) + 2u) + s.bias;
-    if (bound >= 0x7C00u)
-        return fail(MSW_E_RANGE, "match*(len+1)=%llu exceeds the 16-bit score range",
-                    (unsigned long long)bound);
+    (void)s;
+    if (max_m > (uint32_t)msw::kMaxLongLen)
+        return fail(MSW_E_RANGE, "read length %u > %d", max_m, msw::kMaxLongLen);
+    if (max_n > (uint32_t)msw::kMaxLongLen)
+        return fail(MSW_E_RANGE, "window length %u > %d", max_n, msw::kMaxLongLen);
+    return MSW_OK;
+}
+
+// A pair (or a bound) beyond the packed kernels' limits.
+inline bool is_long(uint32_t m, uint32_t n) {
+    return m > (uint32_t)msw::kMaxReadLen || n > (uint32_t)msw::kMaxWinLen;
+}
+
+// Long-pair launch (p's pointers, order and output fields set by the caller):
+// one wave per pair over min(n, 4096) blocks; reads longer than one strip
+// need per-block boundary rows, allocated stream-ordered on `st` so calls on
+// any stream stay independent.
+int launch_long(const Scheme& sch, msw::SwParams p, uint64_t n, uint32_t max_m, uint32_t max_n, hipStream_t st) {
+    if (n == 0) return MSW_OK;
+    p.n_slots = (uint32_t)n;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(n, 4096);
+    int32_t* scratch = nullptr;
+    if (max_m > 64u * (uint32_t)msw::long_rows_per_lane(max_m)) {
+        p.long_cols = msw::long_scratch_cols(max_n);
+        HIP_TRY(hipMallocAsync((void**)&scratch,
+                               (size_t)blocks * p.long_cols * (sch.affine ? 2u : 1u) * sizeof(int32_t), st));
+    }
+    p.long_scratch = scratch;
+    const hipError_t e = msw::launch_sw_long(p, sch.affine, sch.coords, max_m, max_n, blocks, st);
+    if (scratch) HIP_TRY(hipFreeAsync(scratch, st));
+    HIP_TRY(e);
     return MSW_OK;
 }
 
@@ -456,15 +482,18 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
 // inside a bucket by window length, so every wave runs with tight bounds.
 struct Bucket {
     uint32_t begin, count, max_m, max_n;
+    bool long_pairs = false;  // beyond the packed kernels: sw_long_kernel
 };
 
 void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32_t* order,
                   std::vector<Bucket>& buckets) {
     buckets.clear();
-    // key = KR (1..16) * 256 + ceil(n / 16) (<= 256): counting sort.
-    constexpr int kKeys = 17 * 257;
+    // key = KR (1..16) * 257 + ceil(n / 16) (<= 256): counting sort; pairs
+    // beyond the packed kernels' limits share the last key.
+    constexpr int kLongKey = 17 * 257, kKeys = kLongKey + 1;
     std::vector<uint32_t> hist(kKeys + 1, 0);
     auto key_of = [&](uint64_t i) {
+        if (is_long(rlen[i], wlen[i])) return kLongKey;
         const int kr = msw::rows_per_lane(rlen[i], false);
         const int nb = (wlen[i] + 15) / 16;
         return kr * 257 + nb;
@@ -482,7 +511,7 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
     }
     if (n && kmin == kmax) {
         for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
-        buckets.push_back({0, (uint32_t)n, gm, gn});
+        buckets.push_back({0, (uint32_t)n, gm, gn, kmin == kLongKey});
         return;
     }
     for (uint64_t i = 0; i < n; ++i) hist[key_of(i) + 1]++;
@@ -500,12 +529,26 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
         }
         buckets.push_back({b, e - b, mm, mn});
     }
+    if (hist[kLongKey + 1] > hist[kLongKey]) {  // the long pairs: last in slot order
+        const uint32_t b = hist[kLongKey], e = hist[kLongKey + 1];
+        uint32_t mm = 0, mn = 0;
+        for (uint32_t s = b; s < e; ++s) {
+            mm = std::max<uint32_t>(mm, rlen[order[s]]);
+            mn = std::max<uint32_t>(mn, wlen[order[s]]);
+        }
+        buckets.push_back({b, e - b, mm, mn, true});
+    }
+}
+
+// The packed-kernel buckets of a list (all but a trailing long bucket).
+size_t short_buckets(const std::vector<Bucket>& buckets) {
+    return !buckets.empty() && buckets.back().long_pairs ? buckets.size() - 1 : buckets.size();
 }
 
 // One-launch table of a bucket list (msw::MultiTable): heaviest waves first
 // (rows per lane x window steps), so the tail of the grid is short waves.
 void fill_multi(const std::vector<Bucket>& buckets, const Scheme& sch, msw::MultiTable& t) {
-    std::vector<Bucket> bs(buckets);
+    std::vector<Bucket> bs(buckets.begin(), buckets.begin() + short_buckets(buckets));
     auto cost = [](const Bucket& b) { return (uint64_t)msw::rows_per_lane(b.max_m, false) * (b.max_n + 16u); };
     std::stable_sort(bs.begin(), bs.end(), [&](const Bucket& a, const Bucket& b) { return cost(a) > cost(b); });
     memset(&t, 0, sizeof(t));
@@ -531,7 +574,28 @@ bool use_multi(size_t n_buckets) {
 
 int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const std::vector<Bucket>& buckets,
                    bool use_order, uint32_t read_stride, uint32_t win_stride) {
-    if (use_order && use_multi(buckets.size())) {
+    const size_t n_short = short_buckets(buckets);
+    if (n_short < buckets.size()) {  // long pairs: their own launch on the same stream
+        const Bucket& b = buckets.back();
+        msw::SwParams p = base_params(sch);
+        p.reads = s.d_reads;
+        p.wins = s.d_wins;
+        p.read_len = s.d_rlen;
+        p.win_len = s.d_wlen;
+        p.order = use_order ? s.d_order + b.begin : nullptr;
+        p.out_by_slot = use_order ? 1u : 0u;
+        p.out_slot_base = b.begin;
+        p.slot_base = use_order ? 0u : b.begin;
+        p.score = s.d_score;
+        p.end_i = sch.coords ? s.d_ei : nullptr;
+        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.read_stride = read_stride;
+        p.win_stride = win_stride;
+        int rc = launch_long(sch, p, b.count, b.max_m, b.max_n, ctx->compute);
+        if (rc) return rc;
+        if (n_short == 0) return MSW_OK;
+    }
+    if (use_order && use_multi(n_short)) {
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
         p.wins = s.d_wins;
@@ -553,7 +617,8 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
         return MSW_OK;
     }
-    for (const Bucket& b : buckets) {
+    for (size_t bi = 0; bi < n_short; ++bi) {
+        const Bucket& b = buckets[bi];
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
         p.wins = s.d_wins;
@@ -1080,10 +1145,12 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     p.read_stride = b->read_stride;
     p.win_stride = b->win_stride;
     p.n_slots = (uint32_t)b->n_pairs;
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    // bounds past the packed kernels: the whole batch on the long-pair kernel
+    if (is_long(max_read_len, max_win_len)) return launch_long(sch, p, b->n_pairs, max_read_len, max_win_len, st);
     p.lds_stride = msw::stream_stride(max_win_len);
     p.win_vec = msw::vec_ok(p.wins, p.win_stride);
     p.f16_ok = f16_fits(sch, max_read_len, max_win_len) ? 1u : 0u;
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
     const LaunchPlan plan = choose_layout(b->n_pairs, max_read_len, max_win_len, sch, ctx->cu_count);
     p.pairs_blocks = plan.pairs_blocks;
     p.group_lanes = plan.group_lanes;
@@ -1114,6 +1181,9 @@ struct msw_plan {
     bool multi = false;
     msw::MultiTable table{};
     LaunchPlan single{};
+    Bucket shorts{};                  // single (non-multi) launch: the one packed-kernel bucket
+    bool has_long = false;
+    Bucket longs{};                   // pairs beyond the packed kernels (sw_long_kernel)
 };
 
 extern "C" {
@@ -1145,9 +1215,18 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
         std::vector<uint32_t> order(n_pairs);
         std::vector<Bucket> buckets;
         bucket_chunk(read_len, win_len, n_pairs, order.data(), buckets);
-        pl->multi = use_multi(buckets.size());
-        if (pl->multi) fill_multi(buckets, sch, pl->table);
-        else pl->single = choose_layout(n_pairs, gm, gn, sch, ctx->cu_count);
+        const size_t n_short = short_buckets(buckets);
+        if (n_short < buckets.size()) {
+            pl->has_long = true;
+            pl->longs = buckets.back();
+        }
+        pl->multi = use_multi(n_short);
+        if (pl->multi) {
+            fill_multi(buckets, sch, pl->table);
+        } else if (n_short == 1) {
+            pl->shorts = buckets[0];
+            pl->single = choose_layout(pl->shorts.count, pl->shorts.max_m, pl->shorts.max_n, sch, ctx->cu_count);
+        }
         rc = grow_dev(&pl->d_order, n_pairs);
         hipError_t e = rc ? hipSuccess : hipMemcpy(pl->d_order, order.data(), n_pairs * sizeof(uint32_t),
                                                    hipMemcpyHostToDevice);
@@ -1215,18 +1294,26 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
         p.end_i = sch.coords ? t_i : nullptr;
         p.end_j = sch.coords ? t_j : nullptr;
     }
+    if (plan->has_long) {  // the long pairs' slots come last: [longs.begin, n)
+        msw::SwParams q = p;
+        q.order = plan->d_order + plan->longs.begin;
+        q.out_slot_base = plan->longs.begin;
+        q.slot_lens = nullptr;
+        if ((rc = launch_long(sch, q, plan->longs.count, plan->longs.max_m, plan->longs.max_n, st))) return rc;
+    }
     if (plan->multi) {
         p.group_lanes = 16;
         p.groups = 4;
         HIP_TRY(msw::launch_sw_multi(p, plan->table, sch.affine, sch.coords, st));
-    } else {
-        p.n_slots = (uint32_t)plan->n;
-        p.lds_stride = msw::stream_stride(plan->max_n);
-        p.f16_ok = f16_fits(sch, plan->max_m, plan->max_n) ? 1u : 0u;
+    } else if (plan->shorts.count) {  // one packed-kernel bucket: slots [0, count)
+        const Bucket& b = plan->shorts;
+        p.n_slots = b.count;
+        p.lds_stride = msw::stream_stride(b.max_n);
+        p.f16_ok = f16_fits(sch, b.max_m, b.max_n) ? 1u : 0u;
         p.pairs_blocks = plan->single.pairs_blocks;
         p.group_lanes = plan->single.group_lanes;
         p.groups = plan->single.groups;
-        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, plan->max_m, plan->single.layout, st));
+        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan->single.layout, st));
     }
     if (!plan->identity)
         HIP_TRY(msw::launch_gather_results(plan->d_inv, t_score, t_i, t_j, out->score, sch.coords ? out->end_i : nullptr,
@@ -1364,7 +1451,7 @@ int msw_align_reads_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_geno
     if (g->ctx != ctx) return fail(MSW_E_INVALID, "genome belongs to another context");
     if (n == 0) return MSW_OK;
     if (!reads || !read_len || !win_pos || !out || !out->score) return fail(MSW_E_INVALID, "NULL array");
-    if (window > (uint32_t)msw::kMaxWinLen) return fail(MSW_E_RANGE, "window %u > %d", window, msw::kMaxWinLen);
+    if (window > (uint32_t)msw::kMaxLongLen) return fail(MSW_E_RANGE, "window %u > %d", window, msw::kMaxLongLen);
     int rc = set_device(ctx);
     if (rc) return rc;
     const uint32_t max_win = window ? window : std::min<uint32_t>(2u * max_read_len, (uint32_t)msw::kMaxWinLen);

@@ -258,8 +258,26 @@ def test_full_wgs_compat_long_reads(tmp_path):
 
 @pytest.mark.gpu
 def test_pair_sw_oversize_is_range_error(tmp_path):
-    """A 70,000-base sequence must not wrap through the u16 length."""
+    """A 70,000-base sequence must not wrap through the u16 length (ADVICE r1);
+    past 32767 bases it is a range error."""
     r = run(["-1", "A" * 70000, "-2", "ACGT", "--gpu", "--score-mode", "sw"], cwd=tmp_path)
     assert r.returncode == 1 and "exceeds the kernel limits" in r.stderr
-    r = run(["-1", "A" * 300, "-2", "ACGT", "--gpu", "--score-mode", "sw"], cwd=tmp_path)
-    assert r.returncode == 1 and "read length 300" in r.stderr
+    r = run(["-1", "A" * 32768, "-2", "ACGT", "--gpu", "--score-mode", "sw"], cwd=tmp_path)
+    assert r.returncode == 1 and "exceeds the kernel limits" in r.stderr
+
+
+@pytest.mark.gpu
+def test_pair_sw_long_sequences(tmp_path, oracle):
+    """Pair mode with reads past the packed kernels (300 bp read, 5 kb window):
+    the long-pair kernel, checked against the oracle (score and best cell)."""
+    rng = np.random.default_rng(21)
+    alpha = np.frombuffer(b"ACGT", np.uint8)
+    w = rng.choice(alpha, 5000)
+    r = w[1200:1500].copy()
+    r[::37] = ord("A")
+    s1, s2 = bytes(r).decode(), bytes(w).decode()
+    res = run(["-1", s1, "-2", s2, "--gpu", "--score-mode", "sw"], cwd=tmp_path)
+    assert res.returncode == 0, res.stdout + res.stderr
+    ws, wi, wj = oracle.sw_batch(r[None, :], np.array([300], np.uint16), w[None, :], np.array([5000], np.uint16))
+    assert f"GPU Alignment score: {int(ws[0])}" in res.stdout
+    assert f"Best cell: read {int(wi[0])}, window {int(wj[0])}" in res.stdout

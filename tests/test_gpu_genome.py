@@ -260,9 +260,9 @@ def test_error_paths(gpu_ctx):
     from mini_parallel_amd._lib import lib
     g = gpu_ctx.load_genome(b"ACGT" * 100)
     R = np.zeros((2, 16), np.uint8)
-    with pytest.raises(mpa.MswError, match="window length"):  # requested window > 4096
+    with pytest.raises(mpa.MswError, match="window length"):  # requested window > 32767
         gpu_ctx.align_reads(g, R, np.array([4, 4], np.uint16), np.zeros(2, np.int64),
-                            np.array([4097, 4], np.uint16))
+                            np.array([32768, 4], np.uint16))
     with pytest.raises(mpa.MswError, match="unknown ticket"):
         from mini_parallel_amd._lib import check
         check(lib().msw_wait(gpu_ctx.handle, ctypes.c_uint64(10 ** 12)))

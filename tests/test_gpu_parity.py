@@ -249,8 +249,9 @@ def test_empty_batch(gpu_ctx):
 
 @pytest.mark.parametrize("bad", ["long_read", "long_window", "match", "mismatch", "delta"])
 def test_range_errors(gpu_ctx, bad):
-    R, rl, W, wl = mpa.pack_batch([b"A" * 257 if bad == "long_read" else b"ACGT"],
-                                  [b"A" * 4097 if bad == "long_window" else b"ACGT"])
+    # lengths past the long-pair kernel's 32767 (i16 coordinates)
+    R, rl, W, wl = mpa.pack_batch([b"A" * 32768 if bad == "long_read" else b"ACGT"],
+                                  [b"A" * 32768 if bad == "long_window" else b"ACGT"])
     sc = {"match": Scoring(match=65), "mismatch": Scoring(mismatch=1),
           "delta": Scoring(match=10, mismatch=-55)}.get(bad, Scoring())
     with pytest.raises(mpa.MswError):
