@@ -385,7 +385,16 @@ struct Checkpoint {
 // --full-wgs driver: reader threads fill read slabs, a bounded queue hands
 // chunks to one host thread per GPU (own msw_ctx), results are summed per file.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kReadStride = 256;
+// Read slab stride of sw mode: MSW_MAX_READ_LEN (default 256, the packed
+// kernels' read limit; up to 32767 -- longer reads then score on the
+// long-pair kernel and the host reader parses them; the GPU lane reader's
+// slabs stay at <= 256).
+uint32_t read_stride_of_env() {
+    const long v = atol(env_or("MSW_MAX_READ_LEN", "256").c_str());
+    if (v < 1 || v > 32767) die("error: MSW_MAX_READ_LEN must be in [1, 32767]");
+    return std::max<uint32_t>(16u, ((uint32_t)v + 15u) & ~15u);
+}
+const uint32_t kReadStride = read_stride_of_env();
 
 // Read slabs in pinned memory (msw_host_alloc = hipHostMalloc): the FASTQ
 // readers parse straight into them and msw_align_reads DMAs them to the GPU
@@ -646,7 +655,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     // inflate, parse, window cut and scoring run on the worker's GPU
     // (msw_gfastq_* + msw_align_reads_device).  Per-read results come back to
     // the host for the i64 sums and --scores-out, one batch behind the GPU.
-    bool gpu_reader = sw && env_or("MSW_GPU_INFLATE", "1") != "0" && !todo.empty();
+    bool gpu_reader = sw && env_or("MSW_GPU_INFLATE", "1") != "0" && !todo.empty() && kReadStride <= 256;
     for (size_t fi : todo) gpu_reader = gpu_reader && msw_is_bgzf(files[fi].c_str());
     if (gpu_reader) {
         std::atomic<unsigned long long> gz_in{0}, gz_out{0};
@@ -1034,8 +1043,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 else
                     nb = c->cat.size();
                 if (sw) {
-                    // window = reference[pos : pos + W] (W = --window or 2 x read
-                    // length, at most the kernel's 4096), clipped at the genome end
+                    // window = reference[pos : pos + W] (W = --window, at most
+                    // 32767, or 2 x read length capped at 4096), clipped at the genome end
                     std::unique_ptr<InFlight> fl(new InFlight());
                     fl->bases = nb;
                     fl->want.resize(c->n);
@@ -1043,7 +1052,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     fl->ei.assign(c->n, 0);
                     fl->ej.assign(c->n, 0);
                     for (uint64_t i = 0; i < c->n; ++i) {
-                        const uint32_t w = std::min<uint32_t>(a.window > 0 ? (uint32_t)a.window : 2u * c->rlen()[i], 4096u);
+                        const uint32_t w = a.window > 0 ? std::min<uint32_t>((uint32_t)a.window, 32767u)
+                                                        : std::min<uint32_t>(2u * c->rlen()[i], 4096u);
                         fl->want[i] = (uint16_t)w;
                         const int64_t p = c->pos()[i];
                         if (p >= 0 && (uint64_t)p < genome.size())

@@ -141,6 +141,13 @@ int check_bounds(const Scheme& s, uint32_t max_m, uint32_t max_n) {
 inline bool is_long(uint32_t m, uint32_t n) {
     return m > (uint32_t)msw::kMaxReadLen || n > (uint32_t)msw::kMaxWinLen;
 }
+// MSW_FORCE_LONG=1 sends every pair to the long-pair kernel (tests and
+// tools/long_bench.py run it on the packed kernels' shapes); read once per
+// call, like MSW_LAYOUT.
+inline bool force_long() {
+    const char* e = getenv("MSW_FORCE_LONG");
+    return e && *e == '1';
+}
 
 // Long-pair launch (p's pointers, order and output fields set by the caller):
 // one wave per pair over min(n, 4096) blocks; reads longer than one strip
@@ -492,8 +499,9 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
     // beyond the packed kernels' limits share the last key.
     constexpr int kLongKey = 17 * 257, kKeys = kLongKey + 1;
     std::vector<uint32_t> hist(kKeys + 1, 0);
+    const bool all_long = force_long();
     auto key_of = [&](uint64_t i) {
-        if (is_long(rlen[i], wlen[i])) return kLongKey;
+        if (all_long || is_long(rlen[i], wlen[i])) return kLongKey;
         const int kr = msw::rows_per_lane(rlen[i], false);
         const int nb = (wlen[i] + 15) / 16;
         return kr * 257 + nb;
@@ -1147,7 +1155,8 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     p.n_slots = (uint32_t)b->n_pairs;
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
     // bounds past the packed kernels: the whole batch on the long-pair kernel
-    if (is_long(max_read_len, max_win_len)) return launch_long(sch, p, b->n_pairs, max_read_len, max_win_len, st);
+    if (force_long() || is_long(max_read_len, max_win_len))
+        return launch_long(sch, p, b->n_pairs, max_read_len, max_win_len, st);
     p.lds_stride = msw::stream_stride(max_win_len);
     p.win_vec = msw::vec_ok(p.wins, p.win_stride);
     p.f16_ok = f16_fits(sch, max_read_len, max_win_len) ? 1u : 0u;

@@ -146,6 +146,35 @@ def test_full_wgs_sw_and_resume(tmp_path, oracle, bgzf, gpu_inflate):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bgzf", [False, True])
+def test_full_wgs_sw_long_reads(tmp_path, oracle, bgzf):
+    """--full-wgs --score-mode sw with 300 bp reads (MSW_MAX_READ_LEN=300:
+    wider host slabs; BGZF files then take the host reader, the GPU lane
+    reader's slabs being <= 256) scored on the long-pair kernel against
+    600-base windows: per-read records and per-file sums equal the oracle's."""
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=1, reads_per_lane=2, reads_per_file=700, read_len=300,
+                           bgzf=bgzf)
+    env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "1",
+           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "300", "WGS_RUN_ID": "long",
+           "MSW_MAX_READ_LEN": "300"}
+    (tmp_path / "scores").mkdir()
+    r = run(["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "600",
+             "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json"),
+             "--scores-out", str(tmp_path / "scores")], env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = 0
+    for f, b in zip(ds["files"], ds["batches"]):
+        assert int(b.read_len.max()) > 256
+        s, i, j = oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=8)
+        want += int(s.astype(np.int64).sum())
+        got = np.fromfile(tmp_path / "scores" / (os.path.basename(f) + ".scores"), dtype=REC_T)
+        assert np.array_equal(got["score"], s) and np.array_equal(got["end_i"], i) and np.array_equal(got["end_j"], j)
+    rec = json.load(open(tmp_path / "rec.json"))
+    assert rec["total_score"] == want and rec["total_reads"] == 1400 and not rec["gpu_inflate"]
+
+
+@pytest.mark.gpu
 def test_full_wgs_compat_and_test_wgs(tmp_path):
     from mini_parallel_amd.synthetic import write_wgs_dataset
     ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=1, reads_per_lane=2, reads_per_file=95)

@@ -236,3 +236,14 @@ def test_long_genome_reads(gpu_ctx, oracle, kind):
             W[k, :w.size] = w
             eff[k] = w.size
     assert_same(got, oracle_run(oracle, R, rl, W, eff, sc), sc.want_coords)
+
+
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_long_kernel_on_short_shapes(gpu_ctx, oracle, monkeypatch, kind):
+    """MSW_FORCE_LONG=1: the long-pair kernel over the packed kernels' own
+    shapes (config-2 pairs, mixed 75-250 bp reads) -- one strip, R = 1..4."""
+    monkeypatch.setenv("MSW_FORCE_LONG", "1")
+    sc = scoring(kind)
+    for b in (make_pairs(3000, 150, seed=31), make_pairs(2000, (1, 250), seed=32)):
+        assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc),
+                    oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc), sc.want_coords)
