@@ -66,6 +66,10 @@ __global__ __launch_bounds__(64) void sw_long_kernel(SwParams p) {
     const int32_t mismatch = match - (int32_t)(p.delta2 & 0xFFFFu);
     const int32_t gap = (int32_t)(p.gap2 & 0xFFFFu);  // linear gap / affine gap_extend
     const int32_t goe = (int32_t)(p.open_ext2 & 0xFFFFu) - (int32_t)(p.bias2 & 0xFFFFu);
+    // the substitution values live in VGPRs (v_cndmask operands), loaded once
+    int32_t vmatch, vmismatch;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(vmatch) : "s"(match));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(vmismatch) : "s"(mismatch));
     const uint32_t cols = p.long_cols;
     int32_t* const bnd_h = p.long_scratch ? p.long_scratch + (size_t)blockIdx.x * cols * (AFFINE ? 2u : 1u) : nullptr;
     int32_t* const bnd_f = bnd_h ? bnd_h + cols : nullptr;
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(64) void sw_long_kernel(SwParams p) {
         for (int s = 0; s < strips; ++s) {
             const bool bin = s > 0, bout = s + 1 < strips;  // wave-uniform
             const int row0 = s * 64 * R + lane * R;
-            int32_t rb[R], hl[R], ee[R], bs[R], bj[R];
+            int32_t rb[R], hl[R], h2[R], ee[R], bs[R], bj[R];
 #pragma unroll
             for (int k = 0; k < R; ++k) {
                 rb[k] = row0 + k < m ? (int32_t)rd[row0 + k] : kNoMatch;
@@ -107,59 +111,73 @@ __global__ __launch_bounds__(64) void sw_long_kernel(SwParams p) {
                     bi_h = coherent_load(bnd_h + tb + lane);
                     if (AFFINE) bi_f = coherent_load(bnd_f + tb + lane);
                 }
-                auto block = [&](auto mask_tag) __attribute__((always_inline)) {
+                // one step: H of the lane's rows at column t - lane; `in` holds
+                // them at the previous column (left; row k-1's is row k's
+                // diagonal), `out` receives them -- two steps per iteration
+                // swap the arrays instead of copying registers
+                auto step = [&](auto mask_tag, int u, const int32_t(&in)[R], int32_t(&out)[R])
+                                __attribute__((always_inline)) {
                     constexpr bool MASK = decltype(mask_tag)::value;
-                    const int ue = min(64, steps - tb);
-                    for (int u = 0; u < ue; ++u) {
-                        const int t = tb + u;
-                        const int32_t up0 = shr1_or(hb, bi_h);
-                        int32_t fu = kNeg;
-                        if (AFFINE) fu = shr1_or(fb, bi_f);
-                        if (bin) {
-                            bi_h = shl1_or(bi_h, 0);
-                            if (AFFINE) bi_f = shl1_or(bi_f, kNeg);
-                        }
-                        const int j = t - lane;
-                        const int32_t w = lds_win[64 + j];
-                        const bool ok = !MASK || (uint32_t)j < (uint32_t)n;
-                        int32_t up = up0, diag = dg;
-                        dg = up0;
+                    const int t = tb + u;
+                    const int32_t up0 = shr1_or(hb, bi_h);
+                    int32_t fu = kNeg;
+                    if (AFFINE) fu = shr1_or(fb, bi_f);
+                    if (bin) {
+                        bi_h = shl1_or(bi_h, 0);
+                        if (AFFINE) bi_f = shl1_or(bi_f, kNeg);
+                    }
+                    const int j = t - lane;
+                    const int32_t w = lds_win[64 + j];
+                    const bool ok = !MASK || (uint32_t)j < (uint32_t)n;
 #pragma unroll
-                        for (int k = 0; k < R; ++k) {
-                            const int32_t sc = rb[k] == w ? match : mismatch;
-                            int32_t h;
-                            if (AFFINE) {
-                                ee[k] = max(ee[k] - gap, hl[k] - goe);
-                                fu = max(fu - gap, up - goe);
-                                h = max(max(diag + sc, ee[k]), max(fu, 0));
-                            } else {
-                                h = max(max(diag + sc, max(up, hl[k]) - gap), 0);
-                            }
-                            if (MASK) h = ok ? h : 0;
-                            if (COORDS) {
-                                if (h > bs[k]) {
-                                    bs[k] = h;
-                                    bj[k] = j;
-                                }
-                            } else {
-                                best = max(best, h);
-                            }
-                            diag = hl[k];
-                            hl[k] = h;
-                            up = h;
+                    for (int k = 0; k < R; ++k) {
+                        const int32_t diag = k ? in[k - 1] : dg;
+                        const int32_t up = k ? out[k - 1] : up0;
+                        const int32_t sc = rb[k] == w ? vmatch : vmismatch;
+                        int32_t h;
+                        if (AFFINE) {
+                            ee[k] = max(ee[k] - gap, in[k] - goe);
+                            fu = max(fu - gap, up - goe);
+                            h = max(max(diag + sc, ee[k]), max(fu, 0));
+                        } else {
+                            h = max(max(diag + sc, max(up, in[k]) - gap), 0);
                         }
-                        hb = up;
-                        if (AFFINE) fb = fu;
-                        if (bout) {
-                            // lane 63 scored column c = t - 63 of the strip's bottom row
-                            const int c = t - 63;
-                            bo_h = shl1_or(bo_h, hb);
-                            if (AFFINE) bo_f = shl1_or(bo_f, fb);
-                            if ((c & 63) == 63 && c >= 63) {  // lanes hold columns [c - 63, c]
-                                bnd_h[c - 63 + lane] = bo_h;
-                                if (AFFINE) bnd_f[c - 63 + lane] = bo_f;
+                        if (MASK) h = ok ? h : 0;
+                        if (COORDS) {
+                            if (h > bs[k]) {
+                                bs[k] = h;
+                                bj[k] = j;
                             }
+                        } else {
+                            best = max(best, h);
                         }
+                        out[k] = h;
+                    }
+                    dg = up0;
+                    hb = out[R - 1];
+                    if (AFFINE) fb = fu;
+                    if (bout) {
+                        // lane 63 scored column c = t - 63 of the strip's bottom row
+                        const int c = t - 63;
+                        bo_h = shl1_or(bo_h, hb);
+                        if (AFFINE) bo_f = shl1_or(bo_f, fb);
+                        if ((c & 63) == 63 && c >= 63) {  // lanes hold columns [c - 63, c]
+                            bnd_h[c - 63 + lane] = bo_h;
+                            if (AFFINE) bnd_f[c - 63 + lane] = bo_f;
+                        }
+                    }
+                };
+                auto block = [&](auto mask_tag) __attribute__((always_inline)) {
+                    const int ue = min(64, steps - tb);
+                    int u = 0;
+                    for (; u + 1 < ue; u += 2) {
+                        step(mask_tag, u, hl, h2);
+                        step(mask_tag, u + 1, h2, hl);
+                    }
+                    if (u < ue) {
+                        step(mask_tag, u, hl, h2);
+#pragma unroll
+                        for (int k = 0; k < R; ++k) hl[k] = h2[k];
                     }
                 };
                 if (tb >= 63 && tb + 64 <= n) block(std::false_type{});

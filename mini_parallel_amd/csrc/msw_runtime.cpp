@@ -150,15 +150,16 @@ inline bool force_long() {
 }
 
 // Long-pair launch (p's pointers, order and output fields set by the caller):
-// one wave per pair over min(n, 4096) blocks; reads longer than one strip
-// need per-block boundary rows, allocated stream-ordered on `st` so calls on
-// any stream stay independent.
+// one wave per pair, blocks striding over the pairs: up to 16 waves per SIMD
+// when one strip holds every read, 8 when reads need per-block boundary rows
+// (allocated stream-ordered on `st`, so calls on any stream stay independent).
 int launch_long(const Scheme& sch, msw::SwParams p, uint64_t n, uint32_t max_m, uint32_t max_n, hipStream_t st) {
     if (n == 0) return MSW_OK;
     p.n_slots = (uint32_t)n;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(n, 4096);
+    const bool strips = max_m > 64u * (uint32_t)msw::long_rows_per_lane(max_m);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(n, strips ? 8192 : 16384);
     int32_t* scratch = nullptr;
-    if (max_m > 64u * (uint32_t)msw::long_rows_per_lane(max_m)) {
+    if (strips) {
         p.long_cols = msw::long_scratch_cols(max_n);
         HIP_TRY(hipMallocAsync((void**)&scratch,
                                (size_t)blocks * p.long_cols * (sch.affine ? 2u : 1u) * sizeof(int32_t), st));

@@ -9,7 +9,7 @@ OUT=../../tools/_variants
 mkdir -p "$OUT/o_$NAME"
 make -s msw_runtime.o msw_fastq.o msw_gfastq.o >/dev/null
 pids=()
-for f in msw_kernels.hip msw_launch_*.hip msw_inflate.hip msw_parse.hip; do
+for f in msw_kernels.hip msw_launch_*.hip msw_long.hip msw_inflate.hip msw_parse.hip; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include "$@" -c "$f" \
       -o "$OUT/o_$NAME/${f%.hip}.o" &
   pids+=($!)
