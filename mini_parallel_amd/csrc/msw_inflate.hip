@@ -62,13 +62,24 @@ constexpr uint32_t kFastBits = 9;   // lit/len lookup: next 9 stream bits -> up 
 constexpr uint32_t kFastDBits = 7;  // distance lookup
 // lit/len entry: [3:0] bits consumed, [5:4] n literals (their bytes in
 // [31:8]); with n = 0: bit 6 = code longer than kFastBits or invalid
-// (canonical decode), bit 7 = a length code: base length [16:8], extra bits
-// [19:17]; neither = end of block.
+// (canonical decode), bit 7 = a length code; neither = end of block.
+// A length code's entry is laid out for s_bfe_u32, whose control operand is
+// offset [4:0] | width [22:16]: [3:0] code bits L (the extra bits' offset),
+// [13:8] L + extra bits, [22:16] extra bits, [31:23] base length -- the
+// entry itself extracts the extra bits, one SALU op.
 constexpr uint32_t kFastLong = 0x40u;
 constexpr uint32_t kFastMatch = 0x80u;
-// distance entry: [3:0] bits, [7:4] extra bits, [22:8] base distance,
+// distance entry, the same s_bfe_u32 layout: [3:0] code bits, [12:8] code +
+// extra bits, [22:16] extra bits; the base distance sits in fast_dbase;
 // bit 31 = code longer than kFastDBits or invalid
 constexpr uint32_t kFastDLong = 0x80000000u;
+
+// s_bfe_u32 d, v, ctl: (v >> ctl[4:0]) & ((1 << ctl[22:16]) - 1), wave-uniform
+__device__ __forceinline__ uint32_t sbfe(uint32_t v, uint32_t ctl) {
+    uint32_t d;
+    asm("s_bfe_u32 %0, %1, %2" : "=s"(d) : "s"(v), "s"(ctl));
+    return d;
+}
 
 __device__ __forceinline__ uint32_t len_base(uint32_t sym, uint32_t& extra) {
     if (sym < 265) { extra = 0; return sym - 254; }
@@ -98,10 +109,11 @@ struct __align__(16) InflateLds {
         } hdr;
     } u;
     uint32_t fast_d[1u << kFastDBits];
+    uint16_t fast_dbase[1u << kFastDBits];  // base distance of each fast_d entry
     uint16_t sym_ll[288];  // lit/len symbols sorted by (code length, symbol)
     uint16_t sym_d[32];    // distance symbols
 };
-static_assert(sizeof(InflateLds) <= 3328, "inflate tables: <= 3.25 KB of LDS per wave");
+static_assert(sizeof(InflateLds) <= 3584, "inflate tables: <= 3.5 KB of LDS per wave");
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
 // A call's result is divergent to the compiler; every control value of the
@@ -214,7 +226,7 @@ __device__ __noinline__ void build_fast(uint32_t lim_ll, int32_t bas_ll, uint32_
             } else if (s1 >= 257 && s1 <= 285) {
                 uint32_t x;
                 const uint32_t base = len_base(s1, x);
-                e = L1 | kFastMatch | (base << 8) | (x << 17);
+                e = L1 | kFastMatch | ((L1 + x) << 8) | (x << 16) | (base << 23);
             } else if (s1 >= 256) {
                 e = kFastLong;  // 286 / 287: the canonical decode reports it
             } else {
@@ -247,16 +259,17 @@ __device__ __noinline__ void build_fast(uint32_t lim_ll, int32_t bas_ll, uint32_
                 L = (uint32_t)k;
                 B = bd[k];
             }
-        uint32_t e = kFastDLong;
+        uint32_t e = kFastDLong, base = 0;
         if (L) {
             const uint32_t d = S.sym_d[(uint32_t)(B + (int32_t)(r >> (15 - L)))];
             if (d <= 29) {
                 uint32_t x;
-                const uint32_t base = dist_base(d, x);
-                e = L | (x << 4) | (base << 8);
+                base = dist_base(d, x);
+                e = L | ((L + x) << 8) | (x << 16);
             }
         }
         S.fast_d[i] = e;
+        S.fast_dbase[i] = (uint16_t)base;
     }
     __syncthreads();
 }
@@ -563,10 +576,12 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             }
             GZP(4, 1);
             uint32_t len;
-            if (e & kFastMatch) {
-                // a length code from the table: base + extra bits, no branching on the symbol
-                br.drop(e & 15u);
-                len = ((e >> 8) & 0x1FFu) + br.take((e >> 17) & 7u);
+            if (__builtin_expect((e & kFastMatch) != 0, 1)) {
+                // a length code from the table: the entry is the s_bfe
+                // control of its extra bits; base + extra, code + extra dropped
+                // (bcnt >= 32 here: every token starts after a refill)
+                len = (e >> 23) + sbfe((uint32_t)br.bb, e);
+                br.drop(sbfe(e, 0x60008u));
             } else if (!(e & kFastLong)) {
                 br.drop(e & 15u);  // end of block
                 break;
@@ -592,11 +607,12 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 const uint32_t c = br.refill_code();
                 if (c) { err = c; break; }
             }
-            const uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[(uint32_t)br.bb & ((1u << kFastDBits) - 1u)]);
+            const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
+            const uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
             uint32_t dist;
-            if (!(ed & kFastDLong)) {
-                br.drop(ed & 15u);
-                dist = ((ed >> 8) & 0x7FFFu) + br.take((ed >> 4) & 15u);
+            if (__builtin_expect(!(ed & kFastDLong), 1)) {
+                dist = __builtin_amdgcn_readfirstlane((uint32_t)S.fast_dbase[di]) + sbfe((uint32_t)br.bb, ed);
+                br.drop(sbfe(ed, 0x50008u));
             } else {
                 const int ds = decode_sym(br, lim_d, bas_d, S.sym_d);
                 if (ds < 0 || ds > 29) { err = GZ_E_SYMBOL; break; }
@@ -626,9 +642,13 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
                     r += r < 0 ? (int32_t)dist : 0;
                     r -= r >= (int32_t)dist ? (int32_t)dist : 0;
-                    const bool on = j < len;
-                    const uint8_t v = ring[on ? ((opos - dist + (uint32_t)r) & kRingMask) : dummy];
-                    ring[on ? ((opos + j) & kRingMask) : dummy] = v;
+                    // lane select by arithmetic, not a select the compiler
+                    // may turn into an exec-mask branch around the modulo
+                    const uint32_t on = 0u - (uint32_t)(j < len);
+                    const uint32_t src = ((opos - dist + (uint32_t)r) & kRingMask) & on;
+                    const uint32_t dsti = ((opos + j) & kRingMask) & on;
+                    const uint8_t v = ring[src | (dummy & ~on)];
+                    ring[dsti | (dummy & ~on)] = v;
                     j0 += 64;
                 } while (j0 < len);
             } else {
