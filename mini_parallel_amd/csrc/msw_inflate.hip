@@ -73,11 +73,14 @@ constexpr uint32_t kFastMatch = 0x80u;
 // extra bits, [22:16] extra bits; the base distance sits in fast_dbase;
 // bit 31 = code longer than kFastDBits or invalid
 constexpr uint32_t kFastDLong = 0x80000000u;
+// a lit/len "entry" for no code of the set (canonical decode failed)
+constexpr uint32_t kFastBadE = 0x100u;
 
 // s_bfe_u32 d, v, ctl: (v >> ctl[4:0]) & ((1 << ctl[22:16]) - 1), wave-uniform
+// (it also writes SCC, which the compiler must not keep live across it)
 __device__ __forceinline__ uint32_t sbfe(uint32_t v, uint32_t ctl) {
     uint32_t d;
-    asm("s_bfe_u32 %0, %1, %2" : "=s"(d) : "s"(v), "s"(ctl));
+    asm("s_bfe_u32 %0, %1, %2" : "=s"(d) : "s"(v), "s"(ctl) : "scc");
     return d;
 }
 
@@ -547,16 +550,40 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
 #if MSW_GZ_PROFILE
         GZP(1, (uint32_t)(__builtin_amdgcn_s_memtime() - t_hdr));
 #endif
+        // A code longer than the table (or invalid), decoded canonically and
+        // returned as the table entry it would have had (no bits dropped): a
+        // one-literal entry, a length entry, end of block, or kFastBadE --
+        // the token loop then treats it like any table entry.
+        auto slow_ll = [&]() __attribute__((always_inline)) -> uint32_t {
+            const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;  // next 15 bits, first as MSB
+            const uint64_t m = __ballot(r < lim_ll);
+            if (m == 0) return kFastBadE;
+            const uint32_t L = (uint32_t)__builtin_ctzll(m);
+            const int32_t base = __builtin_amdgcn_readlane(bas_ll, (int)L);
+            const uint32_t sym =
+                __builtin_amdgcn_readfirstlane((uint32_t)S.sym_ll[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
+            if (sym < 256) return L | (1u << 4) | (sym << 8);
+            if (sym == 256) return L;
+            if (sym > 285) return kFastBadE;
+            uint32_t x;
+            const uint32_t b = len_base(sym, x);
+            return L | kFastMatch | ((L + x) << 8) | (x << 16) | (b << 23);
+        };
         if (!br.refill()) { err = GZ_E_TRUNC; break; }
         uint32_t ev = lookup();
+        // One exit: every failure lands in `bad` (the literal run masks its
+        // next entry to "not a literal", the match path checks once before
+        // it copies), which keeps the loop free of the exit-selector blocks
+        // a many-exit loop compiles to.  Every token starts with >= 32 bits
+        // in the buffer (a refill follows every drop of a token's last bits).
+        uint32_t bad = 0;
         for (;;) {
             uint32_t e = __builtin_amdgcn_readfirstlane(ev);
-            if ((e >> 4) & 3u) {
+            if (__builtin_expect((e & kFastLong) != 0, 0)) e = slow_ll();
+            if (e & 0x30u) {
                 // Literal runs: a tight inner loop while the lookups yield
                 // literals (1..3 per entry: lane k writes the k-th).
-                // failures clear `ok`, which masks the next entry to "not a
-                // literal": the loop keeps one exit and a one-instruction test
-                uint32_t ok = ~0u, bad = 0;
+                uint32_t ok = ~0u;
                 do {
                     const uint32_t nlit = (e >> 4) & 3u;
                     GZP(2, 1);
@@ -572,58 +599,50 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     if (opos - flushed >= kChunk && !flush_to()) { bad = GZ_E_OVERRUN; ok = 0; }
                     e = __builtin_amdgcn_readfirstlane(ev) & ok;
                 } while (e & 0x30u);
-                if (bad) { err = bad; break; }
+                if (bad) break;
+                continue;  // the next entry is re-dispatched at the top
             }
             GZP(4, 1);
-            uint32_t len;
-            if (__builtin_expect((e & kFastMatch) != 0, 1)) {
-                // a length code from the table: the entry is the s_bfe
-                // control of its extra bits; base + extra, code + extra dropped
-                // (bcnt >= 32 here: every token starts after a refill)
-                len = (e >> 23) + sbfe((uint32_t)br.bb, e);
-                br.drop(sbfe(e, 0x60008u));
-            } else if (!(e & kFastLong)) {
-                br.drop(e & 15u);  // end of block
+            if (!(e & kFastMatch)) {  // end of block, or no code of this set
+                if (e & kFastBadE) bad = GZ_E_SYMBOL;
+                else br.drop(e & 15u);
                 break;
-            } else {
-                // a code longer than the table (or invalid): canonical decode
-                const int sym = decode_sym(br, lim_ll, bas_ll, S.sym_ll);
-                if (sym < 0 || sym > 285) { err = GZ_E_SYMBOL; break; }
-                if (sym < 256) {
-                    if (!br.refill()) { err = GZ_E_TRUNC; break; }
-                    ev = lookup();
-                    ring[lane == 0 ? (opos & kRingMask) : dummy] = (uint8_t)sym;
-                    ++opos;
-                    if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
-                    continue;
-                }
-                if (sym == 256) break;
-                uint32_t x;
-                len = len_base((uint32_t)sym, x);
-                len += br.take(x);
             }
-            // distance
-            if (br.bcnt < 32) {
-                const uint32_t c = br.refill_code();
-                if (c) { err = c; break; }
-            }
+            // a length code: the entry is the s_bfe control of its extra
+            // bits; base + extra, code + extra bits dropped
+            const uint32_t len = (e >> 23) + sbfe((uint32_t)br.bb, e);
+            br.drop(sbfe(e, 0x60008u));
+            if (br.bcnt < 32) bad |= br.refill_code();
+            // distance, the same way (base from the parallel table)
             const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
-            const uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
-            uint32_t dist;
-            if (__builtin_expect(!(ed & kFastDLong), 1)) {
-                dist = __builtin_amdgcn_readfirstlane((uint32_t)S.fast_dbase[di]) + sbfe((uint32_t)br.bb, ed);
-                br.drop(sbfe(ed, 0x50008u));
-            } else {
-                const int ds = decode_sym(br, lim_d, bas_d, S.sym_d);
-                if (ds < 0 || ds > 29) { err = GZ_E_SYMBOL; break; }
-                uint32_t x;
-                dist = dist_base((uint32_t)ds, x);
-                dist += br.take(x);
+            uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
+            uint32_t dbase = __builtin_amdgcn_readfirstlane((uint32_t)S.fast_dbase[di]);
+            if (__builtin_expect((ed & kFastDLong) != 0, 0)) {
+                // longer than the table: canonical decode into an entry
+                const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;
+                const uint64_t m = __ballot(r < lim_d);
+                uint32_t L = 0, d = 31;
+                if (m) {
+                    L = (uint32_t)__builtin_ctzll(m);
+                    const int32_t base = __builtin_amdgcn_readlane(bas_d, (int)L);
+                    d = __builtin_amdgcn_readfirstlane((uint32_t)S.sym_d[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
+                }
+                ed = 0;
+                dbase = 0;
+                if (d > 29) {
+                    bad = GZ_E_SYMBOL;
+                } else {
+                    uint32_t x;
+                    dbase = dist_base(d, x);
+                    ed = L | ((L + x) << 8) | (x << 16);
+                }
             }
-            if (dist > opos) { err = GZ_E_DIST; break; }
-            if (br.bcnt < 32) {
-                const uint32_t c = br.refill_code();
-                if (c) { err = c; break; }
+            const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);
+            br.drop(sbfe(ed, 0x50008u));
+            if (br.bcnt < 32) bad |= br.refill_code();
+            if (__builtin_expect(bad != 0 || dist > opos, 0)) {
+                if (!bad) bad = GZ_E_DIST;
+                break;
             }
             ev = lookup();  // the next token's entry, in flight during the copy
             GZP(5, 1);
@@ -672,7 +691,14 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             GZP(10, (uint32_t)(__builtin_amdgcn_s_memtime() - t_copy));
 #endif
             opos += len;
-            if (opos - flushed >= kChunk && !flush_to()) { err = GZ_E_OVERRUN; break; }
+            if (opos - flushed >= kChunk && !flush_to()) {
+                bad = GZ_E_OVERRUN;
+                break;
+            }
+        }
+        if (bad) {
+            err = bad;
+            break;
         }
     }
     if (err == GZ_OK) {
