@@ -112,11 +112,11 @@ struct __align__(16) InflateLds {
         } hdr;
     } u;
     uint32_t fast_d[1u << kFastDBits];
-    uint16_t fast_dbase[1u << kFastDBits];  // base distance of each fast_d entry
+    uint32_t fast_dbase[1u << kFastDBits];  // base distance of each fast_d entry (u32: one address for both)
     uint16_t sym_ll[288];  // lit/len symbols sorted by (code length, symbol)
     uint16_t sym_d[32];    // distance symbols
 };
-static_assert(sizeof(InflateLds) <= 3584, "inflate tables: <= 3.5 KB of LDS per wave");
+static_assert(sizeof(InflateLds) <= 3712, "inflate tables: <= 3.625 KB of LDS per wave (7 waves per SIMD with the 2 KiB ring)");
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
 // A call's result is divergent to the compiler; every control value of the
@@ -272,7 +272,7 @@ __device__ __noinline__ void build_fast(uint32_t lim_ll, int32_t bas_ll, uint32_
             }
         }
         S.fast_d[i] = e;
-        S.fast_dbase[i] = (uint16_t)base;
+        S.fast_dbase[i] = base;
     }
     __syncthreads();
 }
@@ -610,13 +610,14 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             }
             // a length code: the entry is the s_bfe control of its extra
             // bits; base + extra, code + extra bits dropped
+            // (the first failure of a token is the one reported: bad = bad ? bad : code)
             const uint32_t len = (e >> 23) + sbfe((uint32_t)br.bb, e);
             br.drop(sbfe(e, 0x60008u));
-            if (br.bcnt < 32) bad |= br.refill_code();
+            if (br.bcnt < 32) bad = br.refill_code();  // bad == 0 on entry
             // distance, the same way (base from the parallel table)
             const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
             uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
-            uint32_t dbase = __builtin_amdgcn_readfirstlane((uint32_t)S.fast_dbase[di]);
+            uint32_t dbase = __builtin_amdgcn_readfirstlane(S.fast_dbase[di]);
             if (__builtin_expect((ed & kFastDLong) != 0, 0)) {
                 // longer than the table: canonical decode into an entry
                 const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 ed = 0;
                 dbase = 0;
                 if (d > 29) {
-                    bad = GZ_E_SYMBOL;
+                    bad = bad ? bad : (uint32_t)GZ_E_SYMBOL;
                 } else {
                     uint32_t x;
                     dbase = dist_base(d, x);
@@ -639,11 +640,12 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             }
             const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);
             br.drop(sbfe(ed, 0x50008u));
-            if (br.bcnt < 32) bad |= br.refill_code();
-            if (__builtin_expect(bad != 0 || dist > opos, 0)) {
-                if (!bad) bad = GZ_E_DIST;
-                break;
+            bad = bad ? bad : (dist > opos ? (uint32_t)GZ_E_DIST : 0u);
+            if (br.bcnt < 32) {
+                const uint32_t c = br.refill_code();
+                bad = bad ? bad : c;
             }
+            if (__builtin_expect(bad != 0, 0)) break;
             ev = lookup();  // the next token's entry, in flight during the copy
             GZP(5, 1);
 #if MSW_GZ_PROFILE
