@@ -314,24 +314,20 @@ struct Bits {
         }
         return true;
     }
-    // refill() for loops with a single exit: 0 or GZ_E_TRUNC, never a load past wmax
-    __device__ __forceinline__ uint32_t refill_code() {
-        uint32_t bad = 0;
-        if (bcnt < 32) {
-            if (wi > wmax) {
-                bad = GZ_E_TRUNC;
-            } else {
-                if (wi - wbase >= 64) {
-                    wbase = wi;
-                    cur = src[wbase + lane_id()];
-                }
-                const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(wi - wbase));
-                bb |= (uint64_t)d << bcnt;
-                bcnt += 32;
-                ++wi;
-            }
+    // The token loop's refill (the caller checked bcnt < 32): no truncation
+    // test -- past the member's end it merges whatever follows (window loads
+    // clamped to wmax, so they stay in the buffer); the block loop tests
+    // wi > wmax at every block header, which bounds a runaway decode, and a
+    // member whose decode read past its end reports GZ_E_TRUNC (kernel end).
+    __device__ __forceinline__ void refill_fast() {
+        if (wi - wbase >= 64) {
+            wbase = min(wi, wmax);
+            cur = src[wbase + lane_id()];
         }
-        return bad;
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)((wi - wbase) & 63u));
+        bb |= (uint64_t)d << bcnt;
+        bcnt += 32;
+        ++wi;
     }
     __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
     __device__ __forceinline__ void drop(uint32_t n) {
@@ -425,7 +421,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
 
     bool last = false;
     while (!last && err == GZ_OK) {
-        if (!br.refill()) { err = GZ_E_TRUNC; break; }
+        if (br.wi > br.wmax || !br.refill()) { err = GZ_E_TRUNC; break; }
 #if MSW_GZ_PROFILE
         const uint64_t t_hdr = __builtin_amdgcn_s_memtime();
 #endif
@@ -589,10 +585,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     GZP(2, 1);
                     GZP(3, nlit);
                     br.drop(e & 15u);
-                    if (br.bcnt < 32) {
-                        const uint32_t c = br.refill_code();
-                        if (c) { bad = c; ok = 0; }
-                    }
+                    if (br.bcnt < 32) br.refill_fast();
                     ev = lookup();
                     ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
                     opos += nlit;
@@ -612,8 +605,8 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             // bits; base + extra, code + extra bits dropped
             // (the first failure of a token is the one reported: bad = bad ? bad : code)
             const uint32_t len = (e >> 23) + sbfe((uint32_t)br.bb, e);
-            br.drop(sbfe(e, 0x60008u));
-            if (br.bcnt < 32) bad = br.refill_code();  // bad == 0 on entry
+            br.drop((e >> 8) & 63u);
+            if (br.bcnt < 32) br.refill_fast();
             // distance, the same way (base from the parallel table)
             const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
             uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
@@ -631,7 +624,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 ed = 0;
                 dbase = 0;
                 if (d > 29) {
-                    bad = bad ? bad : (uint32_t)GZ_E_SYMBOL;
+                    bad = GZ_E_SYMBOL;  // bad == 0 on entry
                 } else {
                     uint32_t x;
                     dbase = dist_base(d, x);
@@ -639,12 +632,9 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 }
             }
             const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);
-            br.drop(sbfe(ed, 0x50008u));
+            br.drop((ed >> 8) & 31u);
             bad = bad ? bad : (dist > opos ? (uint32_t)GZ_E_DIST : 0u);
-            if (br.bcnt < 32) {
-                const uint32_t c = br.refill_code();
-                bad = bad ? bad : c;
-            }
+            if (br.bcnt < 32) br.refill_fast();
             if (__builtin_expect(bad != 0, 0)) break;
             ev = lookup();  // the next token's entry, in flight during the copy
             GZP(5, 1);
@@ -703,6 +693,9 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             break;
         }
     }
+    // a decode that ran into the bytes after the member (its last refills
+    // merge them unchecked) failed because the member is truncated
+    if (err != GZ_OK && br.bit_pos() > (mem.coff + mem.clen) * 8u) err = GZ_E_TRUNC;
     if (err == GZ_OK) {
         if (opos > isize) err = GZ_E_OVERRUN;
         else if (opos != isize) err = GZ_E_SIZE;
