@@ -622,7 +622,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     d = __builtin_amdgcn_readfirstlane((uint32_t)S.sym_d[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
                 }
                 ed = 0;
-                dbase = 0;
+                dbase = 0xFFFFFFFFu;  // no code: fails the distance test below, reported as SYMBOL
                 if (d > 29) {
                     bad = GZ_E_SYMBOL;  // bad == 0 on entry
                 } else {
@@ -631,11 +631,13 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     ed = L | ((L + x) << 8) | (x << 16);
                 }
             }
-            const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);
+            const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);  // ed == 0 for no code: dbase
             br.drop((ed >> 8) & 31u);
-            bad = bad ? bad : (dist > opos ? (uint32_t)GZ_E_DIST : 0u);
             if (br.bcnt < 32) br.refill_fast();
-            if (__builtin_expect(bad != 0, 0)) break;
+            if (__builtin_expect(dist > opos, 0)) {  // too far back, or no distance code
+                bad = bad ? bad : (uint32_t)GZ_E_DIST;
+                break;
+            }
             ev = lookup();  // the next token's entry, in flight during the copy
             GZP(5, 1);
 #if MSW_GZ_PROFILE
