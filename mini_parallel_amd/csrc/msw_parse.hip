@@ -124,6 +124,51 @@ __device__ int64_t parse_pos(const uint8_t* s, uint32_t n) {
     return -1;
 }
 
+__constant__ int64_t kPow10[16] = {1ll, 10ll, 100ll, 1000ll, 10000ll, 100000ll, 1000000ll, 10000000ll,
+                                   100000000ll, 1000000000ll, 10000000000ll, 100000000000ll, 1000000000000ll,
+                                   10000000000000ll, 100000000000000ll, 1000000000000000ll};
+
+__device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
+
+// parse_pos of the header [hs, hs + n) by the 16 lanes of a read group (l16 =
+// lane in the group, all 16 active): lane l holds header dwords l..l+2 and
+// tests the four alignments of "pos=" it starts; the first occurrence that
+// a number follows wins (group min); its digits are one byte per lane and
+// the value a group sum of digit x 10^k.  Headers over 60 bytes or numbers
+// of 16+ digits take the serial parse_pos (same result).  buf has >= 72
+// readable bytes past any header start (the span buffer's slack).
+__device__ int64_t group_parse_pos(const uint8_t* buf, uint32_t hs, uint32_t n, uint32_t l16) {
+    if (n > 60) return parse_pos(buf + hs, n);
+    const uint32_t sh = hs & 3u;
+    const uint32_t* p = (const uint32_t*)(buf + (hs - sh)) + l16;
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+    uint32_t best = 0xFFFFu;
+#pragma unroll
+    for (uint32_t s = 0; s < 4; ++s) {
+        const int32_t at = (int32_t)(4u * l16 + s) - (int32_t)sh;  // header offset of this candidate
+        const uint32_t w = __builtin_amdgcn_alignbyte(d1, d0, s);
+        const uint32_t nx = __builtin_amdgcn_alignbyte(d2, d1, s);  // the 4 bytes after it
+        const uint32_t c1 = nx & 0xFFu, c2 = (nx >> 8) & 0xFFu;
+        const bool num = (is_digit(c1) && at + 5 <= (int32_t)n) ||
+                         (c1 == '-' && is_digit(c2) && at + 6 <= (int32_t)n);
+        if (at >= 0 && w == 0x3D736F70u && num) best = min(best, (uint32_t)at);  // "pos="
+    }
+#pragma unroll
+    for (int d = 8; d >= 1; d >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, d, 16));
+    if (best == 0xFFFFu) return -1;
+    const bool neg = buf[hs + best + 4] == '-';
+    const uint32_t q = best + 4u + (neg ? 1u : 0u) + l16;
+    const bool dig = q < n && is_digit(buf[hs + q]);
+    const uint64_t bal = __ballot(dig);
+    const uint32_t mine = (uint32_t)(bal >> (threadIdx.x & 48u)) & 0xFFFFu;  // this group's 16 lanes
+    const uint32_t cnt = (uint32_t)__builtin_ctz(~mine);                    // leading digits (<= 16)
+    if (cnt >= 16) return parse_pos(buf + hs, n);
+    int64_t v = l16 < cnt ? (int64_t)(buf[hs + q] - '0') * kPow10[cnt - 1 - l16] : 0;
+#pragma unroll
+    for (int d = 8; d >= 1; d >>= 1) v += __shfl_xor(v, d, 16);
+    return neg ? -v : v;
+}
+
 // first valid index of a sequence line, given the valid lines before the span
 __device__ __forceinline__ uint32_t seq_phase(uint64_t v0) { return (uint32_t)((5u - (v0 & 3u)) & 3u); }
 
@@ -163,19 +208,51 @@ __global__ __launch_bounds__(256) void k_count(ParseBufs b) {
     }
 }
 
-// 256 threads: a single workgroup that fits on a CU beside inflate waves
+// 256 threads: a single workgroup that fits on a CU beside inflate waves.
+// Thread t owns a contiguous run of tiles (a multiple of 4: 16-byte loads
+// and stores, four in flight per iteration), then adds its block-scan prefix.
 __global__ __launch_bounds__(256) void k_scan_tiles(ParseBufs b) {
     const uint32_t n = b.ntiles, t = threadIdx.x;
-    const uint32_t per = (n + 255) / 256;
+    const uint32_t per = (((n + 255) / 256) + 3u) & ~3u;
     const uint32_t a = min(n, t * per), e = min(n, a + per);
+    const uint32_t e4 = a + ((e - a) & ~3u);
     uint32_t s = 0, h = 0;
-    for (uint32_t i = a; i < e; ++i) {
+    uint32_t i = a;
+    for (; i + 16 <= e4; i += 16) {
+        uint4 v[4], q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = *(const uint4*)(b.tile_nl + i + 4 * k);
+            q[k] = *(const uint4*)(b.tile_hi + i + 4 * k);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s += v[k].x + v[k].y + v[k].z + v[k].w;
+            h |= q[k].x | q[k].y | q[k].z | q[k].w;
+        }
+    }
+    for (; i < e4; i += 4) {
+        const uint4 v = *(const uint4*)(b.tile_nl + i), q = *(const uint4*)(b.tile_hi + i);
+        s += v.x + v.y + v.z + v.w;
+        h |= q.x | q.y | q.z | q.w;
+    }
+    for (; i < e; ++i) {
         s += b.tile_nl[i];
         h |= b.tile_hi[i];
     }
     uint32_t tot;
     uint32_t pre = block_excl_scan<256>(s, &tot);
-    for (uint32_t i = a; i < e; ++i) {
+    for (i = a; i < e4; i += 4) {
+        const uint4 v = *(const uint4*)(b.tile_nl + i);
+        uint4 o;
+        o.x = pre;
+        o.y = o.x + v.x;
+        o.z = o.y + v.y;
+        o.w = o.z + v.z;
+        pre = o.w + v.w;
+        *(uint4*)(b.tile_nl + i) = o;
+    }
+    for (; i < e; ++i) {
         const uint32_t c = b.tile_nl[i];
         b.tile_nl[i] = pre;
         pre += c;
@@ -404,20 +481,16 @@ __global__ __launch_bounds__(256) void k_emit(ParseBufs b, EmitSpan sp, uint64_t
             }
             *(uint4*)(reads + g * b.stride + c0) = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        if (l16 == 0) {
-            rlen[g] = (uint16_t)len;
-            if (pos) {
-                int64_t p = -1;
-                if (j == 0) {
-                    p = sp.pending_in;
-                } else {
-                    const uint64_t kh = ascii ? j - 1 : b.vline[j - 1];
-                    uint32_t hs, he;
-                    line_bounds(b, kh, hs, he);
-                    p = parse_pos(b.buf + hs, he - hs);
-                }
-                pos[g] = p;
+        if (l16 == 0) rlen[g] = (uint16_t)len;
+        if (pos) {  // the header before the sequence line, parsed by the group's 16 lanes
+            int64_t p = sp.pending_in;
+            if (j != 0) {
+                const uint64_t kh = ascii ? j - 1 : b.vline[j - 1];
+                uint32_t hs, he;
+                line_bounds(b, kh, hs, he);
+                p = group_parse_pos(b.buf, hs, he - hs, l16);
             }
+            if (l16 == 0) pos[g] = p;
         }
     }
 }
