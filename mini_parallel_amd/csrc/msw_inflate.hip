@@ -33,6 +33,7 @@
 // Errors follow zlib's inflate (inftrees.c rules for code sets): any error
 // marks the member and stops its wave; no byte is ever written outside the
 // member's ISIZE bytes of output.
+#include <algorithm>
 #include <cstdlib>
 
 #include "msw_gz.h"
@@ -384,8 +385,10 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
     // become unconditional writes whose inactive lanes hit their own dummy
     // byte (a VALU select instead of exec-mask SALU work in the hot loop)
     __shared__ uint32_t ring_words[RING / 4 + 16];
-    const uint32_t m = blockIdx.x;
-    if (m >= n) return;
+    // one member per block, or (a capped grid, launch_gz_inflate) members
+    // blockIdx.x, + gridDim.x, ... in turn: the wave's LDS tables and ring are
+    // rebuilt per member anyway
+    for (uint32_t m = blockIdx.x; m < n; m += gridDim.x) {
     const uint32_t lane = lane_id();
     uint8_t* ring = (uint8_t*)ring_words;
     const uint32_t dummy = RING + lane;  // this lane's dummy byte
@@ -715,9 +718,11 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
     pc[0] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start);
     if (prof && lane == 0)
         for (int i = 0; i < 12; ++i) prof[m * 16 + i] = pc[i];
+    for (int i = 0; i < 12; ++i) pc[i] = 0;
 #else
     (void)prof;
 #endif
+    }  // members
 }
 
 // ---------------------------------------------------------------------------
@@ -844,7 +849,20 @@ hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint
         const char* e = getenv("MSW_GZ_LDS_PAD");
         return e ? (uint32_t)atoi(e) : 0u;
     }();
-#define GZ_LAUNCH(R) hipLaunchKernelGGL(gz_inflate_kernel<R>, dim3(n), dim3(64), lds_pad, stream, cdata, members, n, \
+    // MSW_GZ_WAVES_PER_SIMD: a grid of that many inflate waves per SIMD, each
+    // looping over members, so the rest of every CU (registers, LDS) stays
+    // free for the scoring kernel running beside it (0 = one block per member)
+    static const uint32_t waves_per_simd = [] {
+        const char* e = getenv("MSW_GZ_WAVES_PER_SIMD");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    static const uint32_t simds = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return 4u * (uint32_t)cus;
+    }();
+    const uint32_t grid = waves_per_simd ? std::min<uint32_t>(n, waves_per_simd * simds) : n;
+#define GZ_LAUNCH(R) hipLaunchKernelGGL(gz_inflate_kernel<R>, dim3(grid), dim3(64), lds_pad, stream, cdata, members, n, \
                                          out, status, any_error, prof)
     switch (ring_kb) {
         case 2: GZ_LAUNCH(2048); break;
