@@ -389,338 +389,338 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
     // blockIdx.x, + gridDim.x, ... in turn: the wave's LDS tables and ring are
     // rebuilt per member anyway
     for (uint32_t m = blockIdx.x; m < n; m += gridDim.x) {
-    const uint32_t lane = lane_id();
-    uint8_t* ring = (uint8_t*)ring_words;
-    const uint32_t dummy = RING + lane;  // this lane's dummy byte
-    const uint32_t lit_shift = 8u + 8u * min(lane, 2u);
-    const GzMember mem = members[m];
-    uint8_t* dst = out + mem.ooff;
-    const uint32_t isize = mem.isize;
-    const bool dst_al4 = (mem.ooff & 3) == 0;
+        const uint32_t lane = lane_id();
+        uint8_t* ring = (uint8_t*)ring_words;
+        const uint32_t dummy = RING + lane;  // this lane's dummy byte
+        const uint32_t lit_shift = 8u + 8u * min(lane, 2u);
+        const GzMember mem = members[m];
+        uint8_t* dst = out + mem.ooff;
+        const uint32_t isize = mem.isize;
+        const bool dst_al4 = (mem.ooff & 3) == 0;
 
-    Bits br;
-    br.src = (const uint32_t*)cdata;
-    br.wmax = (uint32_t)((mem.coff + mem.clen) >> 2) + 2u;
-    br.prime(mem.coff);
+        Bits br;
+        br.src = (const uint32_t*)cdata;
+        br.wmax = (uint32_t)((mem.coff + mem.clen) >> 2) + 2u;
+        br.prime(mem.coff);
 
-    uint32_t opos = 0, flushed = 0, err = GZ_OK;
-    uint32_t lim_ll = 0, lim_d = 0, lim_c = 0;
-    int32_t bas_ll = 0, bas_d = 0, bas_c = 0;
-    int tables = -1;  // 1 = fixed tables loaded, 2 = dynamic
+        uint32_t opos = 0, flushed = 0, err = GZ_OK;
+        uint32_t lim_ll = 0, lim_d = 0, lim_c = 0;
+        int32_t bas_ll = 0, bas_d = 0, bas_c = 0;
+        int tables = -1;  // 1 = fixed tables loaded, 2 = dynamic
 
-    // flush [from, from + 256) of the output (ring-resident) to HBM
-    auto flush_chunk = [&](uint32_t from) __attribute__((always_inline)) {
-        const uint32_t v = ring_words[((from + 4u * lane) & kRingMask) >> 2];
-        uint8_t* d = dst + from + 4u * lane;
-        if (dst_al4) {
-            *(uint32_t*)d = v;
-        } else {
-            d[0] = (uint8_t)v;
-            d[1] = (uint8_t)(v >> 8);
-            d[2] = (uint8_t)(v >> 16);
-            d[3] = (uint8_t)(v >> 24);
-        }
-    };
-
-    bool last = false;
-    while (!last && err == GZ_OK) {
-        if (br.wi > br.wmax || !br.refill()) { err = GZ_E_TRUNC; break; }
-#if MSW_GZ_PROFILE
-        const uint64_t t_hdr = __builtin_amdgcn_s_memtime();
-#endif
-        GZP(9, 1);
-        const uint32_t hdr = br.take(3);
-        last = (hdr & 1u) != 0;
-        const uint32_t btype = hdr >> 1;
-        if (btype == 0) {
-            // stored block: byte-align, LEN, NLEN, LEN raw bytes
-            br.drop(br.bcnt & 7u);
-            if (!br.refill()) { err = GZ_E_TRUNC; break; }
-            const uint32_t len = br.take(16), nlen = br.take(16);
-            if (len != (~nlen & 0xFFFFu)) { err = GZ_E_STORED; break; }
-            if (opos + len > isize) { err = GZ_E_OVERRUN; break; }
-            uint32_t k = 0;
-            while (k < len && br.bcnt >= 8) {  // bytes already in the bit buffer
-                const uint32_t v = br.take(8);
-                if (lane == 0) ring[opos & kRingMask] = (uint8_t)v;
-                ++opos;
-                ++k;
-                if ((opos & (kChunk - 1)) == 0) { flush_chunk(opos - kChunk); flushed = opos; }
-            }
-            if (k < len) {
-                // the buffer is empty: the stream continues at byte 4 * wi
-                uint64_t p = (uint64_t)br.wi * 4u;
-                const uint32_t rest = len - k;
-                if (p + rest > mem.coff + mem.clen) { err = GZ_E_TRUNC; break; }
-                for (uint32_t j0 = 0; j0 < rest; j0 += kChunk) {
-                    const uint32_t j = j0 + 4u * lane;
-                    if (j < rest) {
-                        const uint64_t q = p + j;
-                        const uint32_t lo = br.src[q >> 2], hi = br.src[(q >> 2) + 1];
-                        const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(q & 3));
-                        const uint32_t nb = min(4u, rest - j);
-                        // opos already counts the earlier rounds (j0 bytes)
-                        for (uint32_t b = 0; b < nb; ++b)
-                            ring[(opos + 4u * lane + b) & kRingMask] = (uint8_t)(v >> (8 * b));
-                    }
-                    const uint32_t adv = min(kChunk, rest - j0);
-                    opos += adv;
-                    while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
-                }
-                br.prime(p + rest);
-            }
-            continue;
-        }
-        if (btype == 3) { err = GZ_E_BTYPE; break; }
-        if (btype == 1) {
-            if (tables != 1) {
-                for (uint32_t s = lane; s < 288; s += 64)
-                    S.u.hdr.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-                __syncthreads();
-                (void)uni_bool(build_code(S.u.hdr.lens, 288, S.sym_ll, lim_ll, bas_ll, 1));
-                for (uint32_t s = lane; s < 32; s += 64) S.u.hdr.lens[s] = 5;
-                __syncthreads();
-                (void)uni_bool(build_code(S.u.hdr.lens, 32, S.sym_d, lim_d, bas_d, 2));
-                build_fast(lim_ll, bas_ll, lim_d, bas_d, S);
-                tables = 1;
-            }
-        } else {
-            // dynamic block header
-            if (!br.refill()) { err = GZ_E_TRUNC; break; }
-            const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
-            if (nlen > 286 || ndist > 30) { err = GZ_E_HEADER; break; }
-            if (lane < 19) S.u.hdr.lens[lane] = 0;
-            __syncthreads();
-            // code-length code lengths, 3 bits each, in kClOrder (RFC 1951 3.2.7)
-            for (uint32_t i = 0; i < ncode; ++i) {
-                if (!br.refill()) { err = GZ_E_TRUNC; break; }
-                const uint32_t v = br.take(3);
-                if (lane == 0) S.u.hdr.lens[kClOrder[i]] = (uint8_t)v;
-            }
-            if (err) break;
-            __syncthreads();
-            if (!uni_bool(build_code(S.u.hdr.lens, 19, S.u.hdr.sym_c, lim_c, bas_c, 0))) { err = GZ_E_CODES; break; }
-            // lit/len + distance code lengths (one sequence; repeats may cross)
-            const uint32_t total = nlen + ndist;
-            uint32_t idx = 0;
-            while (idx < total) {
-                if (!br.refill()) { err = GZ_E_TRUNC; break; }
-                const int sym = decode_sym(br, lim_c, bas_c, S.u.hdr.sym_c);
-                if (sym < 0) { err = GZ_E_CODES; break; }
-                if (sym < 16) {
-                    if (lane == 0) S.u.hdr.lens[idx] = (uint8_t)sym;
-                    ++idx;
-                    continue;
-                }
-                uint32_t rep, val = 0;
-                if (sym == 16) {
-                    if (idx == 0) { err = GZ_E_HEADER; break; }
-                    val = __builtin_amdgcn_readfirstlane((uint32_t)S.u.hdr.lens[idx - 1]);
-                    rep = 3 + br.take(2);
-                } else if (sym == 17) {
-                    rep = 3 + br.take(3);
-                } else {
-                    rep = 11 + br.take(7);
-                }
-                if (idx + rep > total) { err = GZ_E_HEADER; break; }
-                for (uint32_t k = lane; k < rep; k += 64) S.u.hdr.lens[idx + k] = (uint8_t)val;
-                idx += rep;
-            }
-            if (err) break;
-            __syncthreads();
-            if (__builtin_amdgcn_readfirstlane((uint32_t)S.u.hdr.lens[256]) == 0) { err = GZ_E_CODES; break; }
-            if (!uni_bool(build_code(S.u.hdr.lens, nlen, S.sym_ll, lim_ll, bas_ll, 1))) { err = GZ_E_CODES; break; }
-            if (!uni_bool(build_code(S.u.hdr.lens + nlen, ndist, S.sym_d, lim_d, bas_d, 2))) { err = GZ_E_CODES; break; }
-            build_fast(lim_ll, bas_ll, lim_d, bas_d, S);
-            tables = 2;
-        }
-        // Huffman-coded data until end-of-block.  Token loop with the next
-        // lookup issued before the current token's ring writes / copy, so its
-        // LDS latency overlaps them.  ISIZE is enforced where output leaves
-        // the ring (flush) and at the end; the ring absorbs an overrun.
-        auto lookup = [&]() __attribute__((always_inline)) -> uint32_t {
-            return S.u.fast_ll[(uint32_t)br.bb & ((1u << kFastBits) - 1u)];
-        };
-        auto flush_to = [&]() __attribute__((always_inline)) -> bool {
-            if (opos > isize) return false;
-            while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
-            return true;
-        };
-#if MSW_GZ_PROFILE
-        GZP(1, (uint32_t)(__builtin_amdgcn_s_memtime() - t_hdr));
-#endif
-        // A code longer than the table (or invalid), decoded canonically and
-        // returned as the table entry it would have had (no bits dropped): a
-        // one-literal entry, a length entry, end of block, or kFastBadE --
-        // the token loop then treats it like any table entry.
-        auto slow_ll = [&]() __attribute__((always_inline)) -> uint32_t {
-            const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;  // next 15 bits, first as MSB
-            const uint64_t m = __ballot(r < lim_ll);
-            if (m == 0) return kFastBadE;
-            const uint32_t L = (uint32_t)__builtin_ctzll(m);
-            const int32_t base = __builtin_amdgcn_readlane(bas_ll, (int)L);
-            const uint32_t sym =
-                __builtin_amdgcn_readfirstlane((uint32_t)S.sym_ll[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
-            if (sym < 256) return L | (1u << 4) | (sym << 8);
-            if (sym == 256) return L;
-            if (sym > 285) return kFastBadE;
-            uint32_t x;
-            const uint32_t b = len_base(sym, x);
-            return L | kFastMatch | ((L + x) << 8) | (x << 16) | (b << 23);
-        };
-        if (!br.refill()) { err = GZ_E_TRUNC; break; }
-        uint32_t ev = lookup();
-        // One exit: every failure lands in `bad` (the literal run masks its
-        // next entry to "not a literal", the match path checks once before
-        // it copies), which keeps the loop free of the exit-selector blocks
-        // a many-exit loop compiles to.  Every token starts with >= 32 bits
-        // in the buffer (a refill follows every drop of a token's last bits).
-        uint32_t bad = 0;
-        for (;;) {
-            uint32_t e = __builtin_amdgcn_readfirstlane(ev);
-            if (__builtin_expect((e & kFastLong) != 0, 0)) e = slow_ll();
-            if (e & 0x30u) {
-                // Literal runs: a tight inner loop while the lookups yield
-                // literals (1..3 per entry: lane k writes the k-th).
-                uint32_t ok = ~0u;
-                do {
-                    const uint32_t nlit = (e >> 4) & 3u;
-                    GZP(2, 1);
-                    GZP(3, nlit);
-                    br.drop(e & 15u);
-                    if (br.bcnt < 32) br.refill_fast();
-                    ev = lookup();
-                    ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
-                    opos += nlit;
-                    if (opos - flushed >= kChunk && !flush_to()) { bad = GZ_E_OVERRUN; ok = 0; }
-                    e = __builtin_amdgcn_readfirstlane(ev) & ok;
-                } while (e & 0x30u);
-                if (bad) break;
-                continue;  // the next entry is re-dispatched at the top
-            }
-            GZP(4, 1);
-            if (!(e & kFastMatch)) {  // end of block, or no code of this set
-                if (e & kFastBadE) bad = GZ_E_SYMBOL;
-                else br.drop(e & 15u);
-                break;
-            }
-            // a length code: the entry is the s_bfe control of its extra
-            // bits; base + extra, code + extra bits dropped
-            // (the first failure of a token is the one reported: bad = bad ? bad : code)
-            const uint32_t len = (e >> 23) + sbfe((uint32_t)br.bb, e);
-            br.drop((e >> 8) & 63u);
-            if (br.bcnt < 32) br.refill_fast();
-            // distance, the same way (base from the parallel table)
-            const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
-            uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
-            uint32_t dbase = __builtin_amdgcn_readfirstlane(S.fast_dbase[di]);
-            if (__builtin_expect((ed & kFastDLong) != 0, 0)) {
-                // longer than the table: canonical decode into an entry
-                const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;
-                const uint64_t m = __ballot(r < lim_d);
-                uint32_t L = 0, d = 31;
-                if (m) {
-                    L = (uint32_t)__builtin_ctzll(m);
-                    const int32_t base = __builtin_amdgcn_readlane(bas_d, (int)L);
-                    d = __builtin_amdgcn_readfirstlane((uint32_t)S.sym_d[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
-                }
-                ed = 0;
-                dbase = 0xFFFFFFFFu;  // no code: fails the distance test below, reported as SYMBOL
-                if (d > 29) {
-                    bad = GZ_E_SYMBOL;  // bad == 0 on entry
-                } else {
-                    uint32_t x;
-                    dbase = dist_base(d, x);
-                    ed = L | ((L + x) << 8) | (x << 16);
-                }
-            }
-            const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);  // ed == 0 for no code: dbase
-            br.drop((ed >> 8) & 31u);
-            if (br.bcnt < 32) br.refill_fast();
-            if (__builtin_expect(dist > opos, 0)) {  // too far back, or no distance code
-                bad = bad ? bad : (uint32_t)GZ_E_DIST;
-                break;
-            }
-            ev = lookup();  // the next token's entry, in flight during the copy
-            GZP(5, 1);
-#if MSW_GZ_PROFILE
-            const uint64_t t_copy = __builtin_amdgcn_s_memtime();
-#endif
-            if (dist + len <= kRing) {
-                // ring -> ring, 64 bytes per instruction pair; byte j copies
-                // source byte j mod dist (overlapping copies repeat the last
-                // `dist` bytes; j mod dist = j when dist >= len).  Inactive
-                // lanes move their dummy byte.
-                const float rd = __builtin_amdgcn_rcpf((float)dist);
-                uint32_t j0 = 0;
-                do {
-                    const uint32_t j = j0 + lane;
-                    int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
-                    r += r < 0 ? (int32_t)dist : 0;
-                    r -= r >= (int32_t)dist ? (int32_t)dist : 0;
-                    // lane select by arithmetic, not a select the compiler
-                    // may turn into an exec-mask branch around the modulo
-                    const uint32_t on = 0u - (uint32_t)(j < len);
-                    const uint32_t src = ((opos - dist + (uint32_t)r) & kRingMask) & on;
-                    const uint32_t dsti = ((opos + j) & kRingMask) & on;
-                    const uint8_t v = ring[src | (dummy & ~on)];
-                    ring[dsti | (dummy & ~on)] = v;
-                    j0 += 64;
-                } while (j0 < len);
+        // flush [from, from + 256) of the output (ring-resident) to HBM
+        auto flush_chunk = [&](uint32_t from) __attribute__((always_inline)) {
+            const uint32_t v = ring_words[((from + 4u * lane) & kRingMask) >> 2];
+            uint8_t* d = dst + from + 4u * lane;
+            if (dst_al4) {
+                *(uint32_t*)d = v;
             } else {
-                // further back than the ring: the flushed output in L2 (the
-                // source ends well before `flushed`)
-                GZP(6, 1);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
-                // lane j fetches byte j (the dword holding it; a wave's 64
-                // bytes are a few coalesced lines) -- no per-lane loops
-                uint32_t j0 = 0;
-                do {
-                    const uint32_t j = j0 + lane;
-                    const bool on = j < len;
-                    const uint64_t q = mem.ooff + (uint64_t)(opos - dist + (on ? j : 0u));
-                    const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
-                    ring[on ? ((opos + j) & kRingMask) : dummy] = (uint8_t)(w >> (8u * (uint32_t)(q & 3)));
-                    j0 += 64;
-                } while (j0 < len);
+                d[0] = (uint8_t)v;
+                d[1] = (uint8_t)(v >> 8);
+                d[2] = (uint8_t)(v >> 16);
+                d[3] = (uint8_t)(v >> 24);
             }
+        };
+
+        bool last = false;
+        while (!last && err == GZ_OK) {
+            if (br.wi > br.wmax || !br.refill()) { err = GZ_E_TRUNC; break; }
 #if MSW_GZ_PROFILE
-            GZP(10, (uint32_t)(__builtin_amdgcn_s_memtime() - t_copy));
+            const uint64_t t_hdr = __builtin_amdgcn_s_memtime();
 #endif
-            opos += len;
-            if (opos - flushed >= kChunk && !flush_to()) {
-                bad = GZ_E_OVERRUN;
+            GZP(9, 1);
+            const uint32_t hdr = br.take(3);
+            last = (hdr & 1u) != 0;
+            const uint32_t btype = hdr >> 1;
+            if (btype == 0) {
+                // stored block: byte-align, LEN, NLEN, LEN raw bytes
+                br.drop(br.bcnt & 7u);
+                if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                const uint32_t len = br.take(16), nlen = br.take(16);
+                if (len != (~nlen & 0xFFFFu)) { err = GZ_E_STORED; break; }
+                if (opos + len > isize) { err = GZ_E_OVERRUN; break; }
+                uint32_t k = 0;
+                while (k < len && br.bcnt >= 8) {  // bytes already in the bit buffer
+                    const uint32_t v = br.take(8);
+                    if (lane == 0) ring[opos & kRingMask] = (uint8_t)v;
+                    ++opos;
+                    ++k;
+                    if ((opos & (kChunk - 1)) == 0) { flush_chunk(opos - kChunk); flushed = opos; }
+                }
+                if (k < len) {
+                    // the buffer is empty: the stream continues at byte 4 * wi
+                    uint64_t p = (uint64_t)br.wi * 4u;
+                    const uint32_t rest = len - k;
+                    if (p + rest > mem.coff + mem.clen) { err = GZ_E_TRUNC; break; }
+                    for (uint32_t j0 = 0; j0 < rest; j0 += kChunk) {
+                        const uint32_t j = j0 + 4u * lane;
+                        if (j < rest) {
+                            const uint64_t q = p + j;
+                            const uint32_t lo = br.src[q >> 2], hi = br.src[(q >> 2) + 1];
+                            const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(q & 3));
+                            const uint32_t nb = min(4u, rest - j);
+                            // opos already counts the earlier rounds (j0 bytes)
+                            for (uint32_t b = 0; b < nb; ++b)
+                                ring[(opos + 4u * lane + b) & kRingMask] = (uint8_t)(v >> (8 * b));
+                        }
+                        const uint32_t adv = min(kChunk, rest - j0);
+                        opos += adv;
+                        while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
+                    }
+                    br.prime(p + rest);
+                }
+                continue;
+            }
+            if (btype == 3) { err = GZ_E_BTYPE; break; }
+            if (btype == 1) {
+                if (tables != 1) {
+                    for (uint32_t s = lane; s < 288; s += 64)
+                        S.u.hdr.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                    __syncthreads();
+                    (void)uni_bool(build_code(S.u.hdr.lens, 288, S.sym_ll, lim_ll, bas_ll, 1));
+                    for (uint32_t s = lane; s < 32; s += 64) S.u.hdr.lens[s] = 5;
+                    __syncthreads();
+                    (void)uni_bool(build_code(S.u.hdr.lens, 32, S.sym_d, lim_d, bas_d, 2));
+                    build_fast(lim_ll, bas_ll, lim_d, bas_d, S);
+                    tables = 1;
+                }
+            } else {
+                // dynamic block header
+                if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
+                if (nlen > 286 || ndist > 30) { err = GZ_E_HEADER; break; }
+                if (lane < 19) S.u.hdr.lens[lane] = 0;
+                __syncthreads();
+                // code-length code lengths, 3 bits each, in kClOrder (RFC 1951 3.2.7)
+                for (uint32_t i = 0; i < ncode; ++i) {
+                    if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                    const uint32_t v = br.take(3);
+                    if (lane == 0) S.u.hdr.lens[kClOrder[i]] = (uint8_t)v;
+                }
+                if (err) break;
+                __syncthreads();
+                if (!uni_bool(build_code(S.u.hdr.lens, 19, S.u.hdr.sym_c, lim_c, bas_c, 0))) { err = GZ_E_CODES; break; }
+                // lit/len + distance code lengths (one sequence; repeats may cross)
+                const uint32_t total = nlen + ndist;
+                uint32_t idx = 0;
+                while (idx < total) {
+                    if (!br.refill()) { err = GZ_E_TRUNC; break; }
+                    const int sym = decode_sym(br, lim_c, bas_c, S.u.hdr.sym_c);
+                    if (sym < 0) { err = GZ_E_CODES; break; }
+                    if (sym < 16) {
+                        if (lane == 0) S.u.hdr.lens[idx] = (uint8_t)sym;
+                        ++idx;
+                        continue;
+                    }
+                    uint32_t rep, val = 0;
+                    if (sym == 16) {
+                        if (idx == 0) { err = GZ_E_HEADER; break; }
+                        val = __builtin_amdgcn_readfirstlane((uint32_t)S.u.hdr.lens[idx - 1]);
+                        rep = 3 + br.take(2);
+                    } else if (sym == 17) {
+                        rep = 3 + br.take(3);
+                    } else {
+                        rep = 11 + br.take(7);
+                    }
+                    if (idx + rep > total) { err = GZ_E_HEADER; break; }
+                    for (uint32_t k = lane; k < rep; k += 64) S.u.hdr.lens[idx + k] = (uint8_t)val;
+                    idx += rep;
+                }
+                if (err) break;
+                __syncthreads();
+                if (__builtin_amdgcn_readfirstlane((uint32_t)S.u.hdr.lens[256]) == 0) { err = GZ_E_CODES; break; }
+                if (!uni_bool(build_code(S.u.hdr.lens, nlen, S.sym_ll, lim_ll, bas_ll, 1))) { err = GZ_E_CODES; break; }
+                if (!uni_bool(build_code(S.u.hdr.lens + nlen, ndist, S.sym_d, lim_d, bas_d, 2))) { err = GZ_E_CODES; break; }
+                build_fast(lim_ll, bas_ll, lim_d, bas_d, S);
+                tables = 2;
+            }
+            // Huffman-coded data until end-of-block.  Token loop with the next
+            // lookup issued before the current token's ring writes / copy, so its
+            // LDS latency overlaps them.  ISIZE is enforced where output leaves
+            // the ring (flush) and at the end; the ring absorbs an overrun.
+            auto lookup = [&]() __attribute__((always_inline)) -> uint32_t {
+                return S.u.fast_ll[(uint32_t)br.bb & ((1u << kFastBits) - 1u)];
+            };
+            auto flush_to = [&]() __attribute__((always_inline)) -> bool {
+                if (opos > isize) return false;
+                while (opos - flushed >= kChunk) { flush_chunk(flushed); flushed += kChunk; }
+                return true;
+            };
+#if MSW_GZ_PROFILE
+            GZP(1, (uint32_t)(__builtin_amdgcn_s_memtime() - t_hdr));
+#endif
+            // A code longer than the table (or invalid), decoded canonically and
+            // returned as the table entry it would have had (no bits dropped): a
+            // one-literal entry, a length entry, end of block, or kFastBadE --
+            // the token loop then treats it like any table entry.
+            auto slow_ll = [&]() __attribute__((always_inline)) -> uint32_t {
+                const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;  // next 15 bits, first as MSB
+                const uint64_t m = __ballot(r < lim_ll);
+                if (m == 0) return kFastBadE;
+                const uint32_t L = (uint32_t)__builtin_ctzll(m);
+                const int32_t base = __builtin_amdgcn_readlane(bas_ll, (int)L);
+                const uint32_t sym =
+                    __builtin_amdgcn_readfirstlane((uint32_t)S.sym_ll[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
+                if (sym < 256) return L | (1u << 4) | (sym << 8);
+                if (sym == 256) return L;
+                if (sym > 285) return kFastBadE;
+                uint32_t x;
+                const uint32_t b = len_base(sym, x);
+                return L | kFastMatch | ((L + x) << 8) | (x << 16) | (b << 23);
+            };
+            if (!br.refill()) { err = GZ_E_TRUNC; break; }
+            uint32_t ev = lookup();
+            // One exit: every failure lands in `bad` (the literal run masks its
+            // next entry to "not a literal", the match path checks once before
+            // it copies), which keeps the loop free of the exit-selector blocks
+            // a many-exit loop compiles to.  Every token starts with >= 32 bits
+            // in the buffer (a refill follows every drop of a token's last bits).
+            uint32_t bad = 0;
+            for (;;) {
+                uint32_t e = __builtin_amdgcn_readfirstlane(ev);
+                if (__builtin_expect((e & kFastLong) != 0, 0)) e = slow_ll();
+                if (e & 0x30u) {
+                    // Literal runs: a tight inner loop while the lookups yield
+                    // literals (1..3 per entry: lane k writes the k-th).
+                    uint32_t ok = ~0u;
+                    do {
+                        const uint32_t nlit = (e >> 4) & 3u;
+                        GZP(2, 1);
+                        GZP(3, nlit);
+                        br.drop(e & 15u);
+                        if (br.bcnt < 32) br.refill_fast();
+                        ev = lookup();
+                        ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
+                        opos += nlit;
+                        if (opos - flushed >= kChunk && !flush_to()) { bad = GZ_E_OVERRUN; ok = 0; }
+                        e = __builtin_amdgcn_readfirstlane(ev) & ok;
+                    } while (e & 0x30u);
+                    if (bad) break;
+                    continue;  // the next entry is re-dispatched at the top
+                }
+                GZP(4, 1);
+                if (!(e & kFastMatch)) {  // end of block, or no code of this set
+                    if (e & kFastBadE) bad = GZ_E_SYMBOL;
+                    else br.drop(e & 15u);
+                    break;
+                }
+                // a length code: the entry is the s_bfe control of its extra
+                // bits; base + extra, code + extra bits dropped
+                // (the first failure of a token is the one reported: bad = bad ? bad : code)
+                const uint32_t len = (e >> 23) + sbfe((uint32_t)br.bb, e);
+                br.drop((e >> 8) & 63u);
+                if (br.bcnt < 32) br.refill_fast();
+                // distance, the same way (base from the parallel table)
+                const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
+                uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
+                uint32_t dbase = __builtin_amdgcn_readfirstlane(S.fast_dbase[di]);
+                if (__builtin_expect((ed & kFastDLong) != 0, 0)) {
+                    // longer than the table: canonical decode into an entry
+                    const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;
+                    const uint64_t m = __ballot(r < lim_d);
+                    uint32_t L = 0, d = 31;
+                    if (m) {
+                        L = (uint32_t)__builtin_ctzll(m);
+                        const int32_t base = __builtin_amdgcn_readlane(bas_d, (int)L);
+                        d = __builtin_amdgcn_readfirstlane((uint32_t)S.sym_d[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
+                    }
+                    ed = 0;
+                    dbase = 0xFFFFFFFFu;  // no code: fails the distance test below, reported as SYMBOL
+                    if (d > 29) {
+                        bad = GZ_E_SYMBOL;  // bad == 0 on entry
+                    } else {
+                        uint32_t x;
+                        dbase = dist_base(d, x);
+                        ed = L | ((L + x) << 8) | (x << 16);
+                    }
+                }
+                const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);  // ed == 0 for no code: dbase
+                br.drop((ed >> 8) & 31u);
+                if (br.bcnt < 32) br.refill_fast();
+                if (__builtin_expect(dist > opos, 0)) {  // too far back, or no distance code
+                    bad = bad ? bad : (uint32_t)GZ_E_DIST;
+                    break;
+                }
+                ev = lookup();  // the next token's entry, in flight during the copy
+                GZP(5, 1);
+#if MSW_GZ_PROFILE
+                const uint64_t t_copy = __builtin_amdgcn_s_memtime();
+#endif
+                if (dist + len <= kRing) {
+                    // ring -> ring, 64 bytes per instruction pair; byte j copies
+                    // source byte j mod dist (overlapping copies repeat the last
+                    // `dist` bytes; j mod dist = j when dist >= len).  Inactive
+                    // lanes move their dummy byte.
+                    const float rd = __builtin_amdgcn_rcpf((float)dist);
+                    uint32_t j0 = 0;
+                    do {
+                        const uint32_t j = j0 + lane;
+                        int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
+                        r += r < 0 ? (int32_t)dist : 0;
+                        r -= r >= (int32_t)dist ? (int32_t)dist : 0;
+                        // lane select by arithmetic, not a select the compiler
+                        // may turn into an exec-mask branch around the modulo
+                        const uint32_t on = 0u - (uint32_t)(j < len);
+                        const uint32_t src = ((opos - dist + (uint32_t)r) & kRingMask) & on;
+                        const uint32_t dsti = ((opos + j) & kRingMask) & on;
+                        const uint8_t v = ring[src | (dummy & ~on)];
+                        ring[dsti | (dummy & ~on)] = v;
+                        j0 += 64;
+                    } while (j0 < len);
+                } else {
+                    // further back than the ring: the flushed output in L2 (the
+                    // source ends well before `flushed`)
+                    GZP(6, 1);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
+                    // lane j fetches byte j (the dword holding it; a wave's 64
+                    // bytes are a few coalesced lines) -- no per-lane loops
+                    uint32_t j0 = 0;
+                    do {
+                        const uint32_t j = j0 + lane;
+                        const bool on = j < len;
+                        const uint64_t q = mem.ooff + (uint64_t)(opos - dist + (on ? j : 0u));
+                        const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
+                        ring[on ? ((opos + j) & kRingMask) : dummy] = (uint8_t)(w >> (8u * (uint32_t)(q & 3)));
+                        j0 += 64;
+                    } while (j0 < len);
+                }
+#if MSW_GZ_PROFILE
+                GZP(10, (uint32_t)(__builtin_amdgcn_s_memtime() - t_copy));
+#endif
+                opos += len;
+                if (opos - flushed >= kChunk && !flush_to()) {
+                    bad = GZ_E_OVERRUN;
+                    break;
+                }
+            }
+            if (bad) {
+                err = bad;
                 break;
             }
         }
-        if (bad) {
-            err = bad;
-            break;
+        // a decode that ran into the bytes after the member (its last refills
+        // merge them unchecked) failed because the member is truncated
+        if (err != GZ_OK && br.bit_pos() > (mem.coff + mem.clen) * 8u) err = GZ_E_TRUNC;
+        if (err == GZ_OK) {
+            if (opos > isize) err = GZ_E_OVERRUN;
+            else if (opos != isize) err = GZ_E_SIZE;
+            else if ((br.bit_pos() - mem.coff * 8u + 7u) / 8u > mem.clen) err = GZ_E_TRUNC;
         }
-    }
-    // a decode that ran into the bytes after the member (its last refills
-    // merge them unchecked) failed because the member is truncated
-    if (err != GZ_OK && br.bit_pos() > (mem.coff + mem.clen) * 8u) err = GZ_E_TRUNC;
-    if (err == GZ_OK) {
-        if (opos > isize) err = GZ_E_OVERRUN;
-        else if (opos != isize) err = GZ_E_SIZE;
-        else if ((br.bit_pos() - mem.coff * 8u + 7u) / 8u > mem.clen) err = GZ_E_TRUNC;
-    }
-    if (err == GZ_OK) {
-        // the last partial chunk
-        for (uint32_t k = lane; k < opos - flushed; k += 64) dst[flushed + k] = ring[(flushed + k) & kRingMask];
-    }
-    if (lane == 0) {
-        status[m] = err;
-        if (err) atomicOr(any_error, 1u);
-    }
+        if (err == GZ_OK) {
+            // the last partial chunk
+            for (uint32_t k = lane; k < opos - flushed; k += 64) dst[flushed + k] = ring[(flushed + k) & kRingMask];
+        }
+        if (lane == 0) {
+            status[m] = err;
+            if (err) atomicOr(any_error, 1u);
+        }
 #if MSW_GZ_PROFILE
-    pc[0] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start);
-    if (prof && lane == 0)
-        for (int i = 0; i < 12; ++i) prof[m * 16 + i] = pc[i];
-    for (int i = 0; i < 12; ++i) pc[i] = 0;
+        pc[0] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start);
+        if (prof && lane == 0)
+            for (int i = 0; i < 12; ++i) prof[m * 16 + i] = pc[i];
+        for (int i = 0; i < 12; ++i) pc[i] = 0;
 #else
-    (void)prof;
+        (void)prof;
 #endif
     }  // members
 }
