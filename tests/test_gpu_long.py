@@ -247,3 +247,21 @@ def test_long_kernel_on_short_shapes(gpu_ctx, oracle, monkeypatch, kind):
     for b in (make_pairs(3000, 150, seed=31), make_pairs(2000, (1, 250), seed=32)):
         assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc),
                     oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc), sc.want_coords)
+
+
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_long_random_sizes(gpu_ctx, oracle, kind):
+    """240 pairs of random sizes (reads 1..3000, windows 1..5000; related and
+    unrelated), short and long mixed in one call, chunked."""
+    sc = scoring(kind)
+    rng = np.random.default_rng(77)
+    pairs = []
+    for _ in range(240):
+        m, n = int(rng.integers(1, 3001)), int(rng.integers(1, 5001))
+        if rng.random() < 0.2:
+            pairs.append((ACGT[rng.integers(0, 4, m)].tobytes(), ACGT[rng.integers(0, 4, n)].tobytes()))
+        else:
+            pairs.append(related(rng, m, n))
+    R, rl, W, wl = mpa.pack_batch([p[0] for p in pairs], [p[1] for p in pairs])
+    want = oracle_run(oracle, R, rl, W, wl, sc)
+    assert_same(gpu_ctx.align_batch(R, rl, W, wl, sc, chunk_pairs=100), want, sc.want_coords)
