@@ -269,3 +269,22 @@ def test_reader_rejects_plain_gzip(gpu_ctx, tmp_path):
     p.write_bytes(gzip.compress(fastq_text(10, 1)))
     with pytest.raises(MswError, match="BGZF"):
         GpuFastqReader(gpu_ctx, str(p))
+
+
+@pytest.mark.parametrize("cut", [1, 2, 7, 40, 300])
+def test_inflate_truncated_deflate_stream(gpu_ctx, cut):
+    """A member whose deflate data is cut short (BSIZE, CRC and ISIZE left
+    consistent with the shorter member): the decode runs into the trailer
+    and the next member's bytes, which the token loop merges unchecked, and
+    must still report truncation -- zlib says the stream is incomplete."""
+    data = fastq_text(300, 21)[:60000]
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    cdata = c.compress(data) + c.flush()
+    short = cdata[:len(cdata) - cut]
+    with pytest.raises(zlib.error):
+        zlib.decompress(short, -15)
+    member = (struct.pack("<4BIBBH2BHH", 0x1F, 0x8B, 8, 4, 0, 0, 0xFF, 6, ord("B"), ord("C"), 2, len(short) + 25)
+              + short + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data)))
+    blob = member + bgzf_compress(fastq_text(40, 22), 6)  # another member follows
+    with pytest.raises(MswError, match="truncated deflate data"):
+        bgzf_inflate(gpu_ctx, blob)
