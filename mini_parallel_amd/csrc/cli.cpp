@@ -389,17 +389,20 @@ struct Checkpoint {
 // kernels' read limit; up to 32767 -- longer reads then score on the
 // long-pair kernel and the host reader parses them; the GPU lane reader's
 // slabs stay at <= 256).
-uint32_t read_stride_of_env() {
-    const long v = atol(env_or("MSW_MAX_READ_LEN", "256").c_str());
-    if (v < 1 || v > 32767) die("error: MSW_MAX_READ_LEN must be in [1, 32767]");
-    return std::max<uint32_t>(16u, ((uint32_t)v + 15u) & ~15u);
+// (read on first use, so a bad value fails the run that needs it, not --help)
+uint32_t read_stride() {
+    static const uint32_t stride = [] {
+        const long v = atol(env_or("MSW_MAX_READ_LEN", "256").c_str());
+        if (v < 1 || v > 32767) die("error: MSW_MAX_READ_LEN must be in [1, 32767]");
+        return std::max<uint32_t>(16u, ((uint32_t)v + 15u) & ~15u);
+    }();
+    return stride;
 }
-const uint32_t kReadStride = read_stride_of_env();
 
 // Read slabs in pinned memory (msw_host_alloc = hipHostMalloc): the FASTQ
 // readers parse straight into them and msw_align_reads DMAs them to the GPU
 // without staging.  Recycled through a free list; one block per slab:
-// [reads cap x kReadStride | pos i64 x cap | rlen u16 x cap].
+// [reads cap x read_stride() | pos i64 x cap | rlen u16 x cap].
 class SlabPool {
    public:
     struct Slab {
@@ -423,14 +426,14 @@ class SlabPool {
             }
         }
         Slab* s = new Slab();
-        const size_t bytes = cap_ * (kReadStride + 8 + 2);
+        const size_t bytes = cap_ * (read_stride() + 8 + 2);
         s->base = (uint8_t*)msw_host_alloc(bytes);
         s->pinned = s->base != nullptr;
         if (!s->base) s->base = (uint8_t*)malloc(bytes);  // pageable fallback: staged by the runtime
         if (!s->base) die("error: out of host memory for read slabs");
         s->reads = s->base;
-        s->pos = (int64_t*)(s->base + cap_ * kReadStride);
-        s->rlen = (uint16_t*)(s->base + cap_ * (kReadStride + 8));
+        s->pos = (int64_t*)(s->base + cap_ * read_stride());
+        s->rlen = (uint16_t*)(s->base + cap_ * (read_stride() + 8));
         return s;
     }
     void put(Slab* s) {
@@ -452,7 +455,7 @@ class SlabPool {
 struct Chunk {
     size_t file_index = 0;
     SlabPool* pool = nullptr;
-    SlabPool::Slab* slab = nullptr;  // sw: reads n x kReadStride, rlen, pos
+    SlabPool::Slab* slab = nullptr;  // sw: reads n x read_stride(), rlen, pos
     std::vector<uint8_t> cat;        // compat: the chunk's sequences back to back (any read length)
     uint64_t n = 0;
     uint64_t first_read = 0;         // index of the chunk's first read in its file
@@ -655,7 +658,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     // inflate, parse, window cut and scoring run on the worker's GPU
     // (msw_gfastq_* + msw_align_reads_device).  Per-read results come back to
     // the host for the i64 sums and --scores-out, one batch behind the GPU.
-    bool gpu_reader = sw && env_or("MSW_GPU_INFLATE", "1") != "0" && !todo.empty() && kReadStride <= 256;
+    bool gpu_reader = sw && env_or("MSW_GPU_INFLATE", "1") != "0" && !todo.empty() && read_stride() <= 256;
     for (size_t fi : todo) gpu_reader = gpu_reader && msw_is_bgzf(files[fi].c_str());
     if (gpu_reader) {
         std::atomic<unsigned long long> gz_in{0}, gz_out{0};
@@ -752,7 +755,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 };
                 int cur = 0;
                 msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
-                if (msw_gfastq_open(ctx.h, nullptr, kReadStride, batch, 1, 0, &gr) != MSW_OK)
+                if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
                     die(std::string("GPU lane reader: ") + msw_last_error());
                 // the reader's stats of the file it just finished
                 auto reader_done = [&](size_t fi) {
@@ -933,7 +936,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     if (sw) {
                         c->pool = &slabs;
                         c->slab = slabs.get();
-                        ok = msw_fastq_next(fq, c->slab->reads, c->slab->rlen, kReadStride, chunk, &c->n,
+                        ok = msw_fastq_next(fq, c->slab->reads, c->slab->rlen, read_stride(), chunk, &c->n,
                                             c->slab->pos) == MSW_OK;
                     } else {
                         // compat: exactly `chunk` reads of any length, concatenated
@@ -1059,7 +1062,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         if (p >= 0 && (uint64_t)p < genome.size())
                             fl->cells += (unsigned long long)std::min<uint64_t>(w, genome.size() - (uint64_t)p) * c->rlen()[i];
                     }
-                    msw_read_batch_t rb{c->reads(), c->rlen(), kReadStride, c->pos(), fl->want.data(), c->n};
+                    msw_read_batch_t rb{c->reads(), c->rlen(), read_stride(), c->pos(), fl->want.data(), c->n};
                     msw_out_t o{fl->score.data(), fl->ei.data(), fl->ej.data()};
                     fl->c = std::move(c);
                     if (msw_align_reads_async(ctx.h, &sc, gen, &rb, &o, 0, &fl->ticket) != MSW_OK) {
