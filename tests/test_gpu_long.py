@@ -265,3 +265,24 @@ def test_long_random_sizes(gpu_ctx, oracle, kind):
     R, rl, W, wl = mpa.pack_batch([p[0] for p in pairs], [p[1] for p in pairs])
     want = oracle_run(oracle, R, rl, W, wl, sc)
     assert_same(gpu_ctx.align_batch(R, rl, W, wl, sc, chunk_pairs=100), want, sc.want_coords)
+
+
+@pytest.mark.parametrize("env", [{"MSW_NO_MULTI": "1"}, {"MSW_LAYOUT": "split"}, {"MSW_LAYOUT": "pairs", "MSW_GROUP_LANES": "12"},
+                                 {"MSW_NO_F16": "1"}])
+def test_long_beside_forced_layouts(gpu_ctx, oracle, monkeypatch, env):
+    """The long bucket next to per-bucket launches of the packed kernels
+    (forced layouts, no single multi launch) and next to the integer path."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = scoring("linear_coords")
+    rng = np.random.default_rng(5)
+    s = make_pairs(600, (60, 250), seed=9)
+    reads = [bytes(s.reads[k, :s.read_len[k]]) for k in range(s.n_pairs)]
+    wins = [bytes(s.wins[k, :s.win_len[k]]) for k in range(s.n_pairs)]
+    for m, n in EDGE:
+        r, w = related(rng, m, n)
+        at = int(rng.integers(0, len(reads) + 1))
+        reads.insert(at, r)
+        wins.insert(at, w)
+    R, rl, W, wl = mpa.pack_batch(reads, wins)
+    assert_same(gpu_ctx.align_batch(R, rl, W, wl, sc, chunk_pairs=300), oracle_run(oracle, R, rl, W, wl, sc), True)
