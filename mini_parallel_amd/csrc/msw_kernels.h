@@ -156,8 +156,8 @@ hipError_t launch_gather_results(const uint32_t* inv, const int32_t* src_score, 
                                  const int16_t* src_j, int32_t* score, int16_t* end_i, int16_t* end_j, uint64_t n,
                                  hipStream_t stream);
 
-// Long pairs: R = rows per lane for a read-length bound (one strip of 64 * R
-// rows when it fits, else strips of 512); scratch columns per block; LDS bytes.
+// Long pairs: R = rows per lane for a read-length bound (the fewest strips of
+// <= 512 rows, rows spread evenly over them); scratch columns per block; LDS bytes.
 int long_rows_per_lane(uint32_t max_read_len);
 uint32_t long_scratch_cols(uint32_t max_win_len);
 size_t long_lds_bytes(uint32_t max_win_len);

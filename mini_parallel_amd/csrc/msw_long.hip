@@ -244,7 +244,14 @@ hipError_t go(const SwParams& p, bool affine, bool coords, uint32_t blocks, size
 }  // namespace
 
 int long_rows_per_lane(uint32_t max_read_len) {
-    const uint32_t r = (max_read_len + 63) / 64;
+    // as few strips of <= 64 * kLongMaxR rows as the longest read needs, its
+    // rows spread evenly over them: 600 rows -> two strips of 320 (R = 5),
+    // not 512 + 88, which also fits a 300-row read into one strip at 94 %.
+    // (Bucketing long pairs by their own R measured slower: one launch per
+    // R leaves each launch too few waves, tools/long_bench.py mixed case.)
+    const uint32_t m = max_read_len ? max_read_len : 1u;
+    const uint32_t strips = (m + 64u * kLongMaxR - 1) / (64u * kLongMaxR);
+    const uint32_t r = (m + 64u * strips - 1) / (64u * strips);
     return r < 1 ? 1 : (r > (uint32_t)kLongMaxR ? kLongMaxR : (int)r);
 }
 

@@ -27,7 +27,7 @@ def main():
     kinds = {"linear": Scoring(), "affine_coords": Scoring(affine=True, gap_open=3, gap_extend=1, want_coords=True)}
     cases = [("300x600", 40_000, 300, 2.0, False), ("1000x2000", 4_000, 1000, 2.0, False),
              ("150x5000", 8_000, 150, 5000 / 150, False), ("150x300_forced", 10_000, 150, 2.0, True),
-             ("150x300_packed", 10_000, 150, 2.0, False)]
+             ("150x300_packed", 10_000, 150, 2.0, False), ("mixed_257-2000x2", 8_000, (257, 2000), 2.0, False)]
     for name, n, m, wf, force in cases:
         b = make_pairs(n, m, win_factor=wf, seed=4242)
         t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
@@ -36,13 +36,20 @@ def main():
         ei = torch.zeros(n, dtype=torch.int16, device=dev)
         ej = torch.zeros(n, dtype=torch.int16, device=dev)
         cells = float((b.read_len.astype(np.int64) * b.win_len).sum())
+        mixed = isinstance(m, tuple)
         if force:
             os.environ["MSW_FORCE_LONG"] = "1"
         for kname, sc in kinds.items():
-            launch = ctx.prepare_device_launch(t[0].data_ptr(), t[2].data_ptr(), t[1].data_ptr(), t[3].data_ptr(),
-                                               b.reads.shape[1], b.wins.shape[1], n, score.data_ptr(),
-                                               int(b.read_len.max()), int(b.win_len.max()), sc, ei.data_ptr(),
-                                               ej.data_ptr(), stream=st.cuda_stream)
+            if mixed:  # mixed lengths: a plan (length buckets, one launch per long-pair R)
+                launch = ctx.prepare_planned_launch(t[0].data_ptr(), t[2].data_ptr(), t[1].data_ptr(),
+                                                    t[3].data_ptr(), b.reads.shape[1], b.wins.shape[1], b.read_len,
+                                                    b.win_len, score.data_ptr(), sc, ei.data_ptr(), ej.data_ptr(),
+                                                    stream=st.cuda_stream)
+            else:
+                launch = ctx.prepare_device_launch(t[0].data_ptr(), t[2].data_ptr(), t[1].data_ptr(),
+                                                   t[3].data_ptr(), b.reads.shape[1], b.wins.shape[1], n,
+                                                   score.data_ptr(), int(b.read_len.max()), int(b.win_len.max()), sc,
+                                                   ei.data_ptr(), ej.data_ptr(), stream=st.cuda_stream)
             for _ in range(3):
                 launch()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
