@@ -80,7 +80,7 @@ typedef struct {
 /* is path a BGZF file (first member has the 'BC' extra field)? 1 / 0 */
 int msw_is_bgzf(const char* path);
 
-/* read_stride: multiple of 16, <= 256 (longer sequences are MSW_E_RANGE);
+/* read_stride: multiple of 16, <= 32768 (longer sequences are MSW_E_RANGE);
  * max_reads: batch size (device slabs for two batches are allocated);
  * span_bytes: decompressed bytes inflated and parsed per step (0 = default
  * 1 GiB, env MSW_GFASTQ_SPAN_MB).  path may be NULL: the buffers are

@@ -387,8 +387,7 @@ struct Checkpoint {
 // ---------------------------------------------------------------------------
 // Read slab stride of sw mode: MSW_MAX_READ_LEN (default 256, the packed
 // kernels' read limit; up to 32767 -- longer reads then score on the
-// long-pair kernel and the host reader parses them; the GPU lane reader's
-// slabs stay at <= 256).
+// long-pair kernel, with either lane reader).
 // (read on first use, so a bad value fails the run that needs it, not --help)
 uint32_t read_stride() {
     static const uint32_t stride = [] {
@@ -658,12 +657,15 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     // inflate, parse, window cut and scoring run on the worker's GPU
     // (msw_gfastq_* + msw_align_reads_device).  Per-read results come back to
     // the host for the i64 sums and --scores-out, one batch behind the GPU.
-    bool gpu_reader = sw && env_or("MSW_GPU_INFLATE", "1") != "0" && !todo.empty() && read_stride() <= 256;
+    bool gpu_reader = sw && env_or("MSW_GPU_INFLATE", "1") != "0" && !todo.empty();
     for (size_t fi : todo) gpu_reader = gpu_reader && msw_is_bgzf(files[fi].c_str());
     if (gpu_reader) {
         std::atomic<unsigned long long> gz_in{0}, gz_out{0};
+        // reads per scoring launch; wide slabs (MSW_MAX_READ_LEN) keep a batch's
+        // slab near 256 MiB (two per worker)
         const uint64_t batch = std::max<uint64_t>(
-            chunk, strtoull(env_or("MSW_GFASTQ_BATCH", std::to_string(1u << 20)).c_str(), nullptr, 10));
+            chunk, std::min<uint64_t>(strtoull(env_or("MSW_GFASTQ_BATCH", std::to_string(1u << 20)).c_str(), nullptr, 10),
+                                      (256ull << 20) / read_stride()));
         std::atomic<size_t> next_file{0};
         std::vector<std::thread> workers;
         // two workers (contexts) per GPU by default: one file's inflate and

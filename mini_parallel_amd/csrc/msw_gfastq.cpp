@@ -575,8 +575,8 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
                     uint64_t span_bytes, msw_gfastq** out) {
     if (!ctx || !out) return set_error(MSW_E_INVALID, "ctx/out is NULL");
     *out = nullptr;
-    if (read_stride == 0 || read_stride % 16 || read_stride > 256)
-        return set_error(MSW_E_INVALID, "read_stride %u must be a multiple of 16 in [16, 256]", read_stride);
+    if (read_stride == 0 || read_stride % 16 || read_stride > 32768)
+        return set_error(MSW_E_INVALID, "read_stride %u must be a multiple of 16 in [16, 32768]", read_stride);
     if (max_reads == 0) return set_error(MSW_E_INVALID, "max_reads is 0");
     msw_gfastq* g = new msw_gfastq();
     g->ctx = ctx;

@@ -457,7 +457,7 @@ __global__ __launch_bounds__(256) void k_emit(ParseBufs b, EmitSpan sp, uint64_t
     const bool ascii = !sp.any_high;
     const uint64_t v0 = sp.v0;
     const uint32_t ph = seq_phase(v0);
-    const uint32_t l16 = threadIdx.x & 15, c0 = 16u * l16;
+    const uint32_t l16 = threadIdx.x & 15;
     const uint64_t ng = (uint64_t)gridDim.x * 16;
     for (uint64_t g = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 4; g < count; g += ng) {
         const uint64_t j = ph + 4 * (r_begin + g);
@@ -466,7 +466,8 @@ __global__ __launch_bounds__(256) void k_emit(ParseBufs b, EmitSpan sp, uint64_t
         line_bounds(b, k, st, en);
         uint32_t len = en - st;
         if (len > b.stride) len = 0;  // the span is flagged too_long; the host fails the file
-        if (c0 < b.stride) {
+        // 256 bytes of the row per pass of the group's 16 lanes (strides > 256: long reads)
+        for (uint32_t c0 = 16u * l16; c0 < b.stride; c0 += 256u) {
             uint32_t w[4] = {0, 0, 0, 0};
             if (c0 < len) {
                 const uint64_t a = (uint64_t)st + c0;

@@ -149,9 +149,9 @@ def test_full_wgs_sw_and_resume(tmp_path, oracle, bgzf, gpu_inflate):
 @pytest.mark.parametrize("bgzf", [False, True])
 def test_full_wgs_sw_long_reads(tmp_path, oracle, bgzf):
     """--full-wgs --score-mode sw with 300 bp reads (MSW_MAX_READ_LEN=300:
-    wider host slabs; BGZF files then take the host reader, the GPU lane
-    reader's slabs being <= 256) scored on the long-pair kernel against
-    600-base windows: per-read records and per-file sums equal the oracle's."""
+    320-byte slabs; gzip lane files on the host reader, BGZF ones on the GPU
+    lane reader) scored on the long-pair kernel against 600-base windows:
+    per-read records and per-file sums equal the oracle's."""
     from mini_parallel_amd.synthetic import write_wgs_dataset
     ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=1, reads_per_lane=2, reads_per_file=700, read_len=300,
                            bgzf=bgzf)
@@ -171,7 +171,7 @@ def test_full_wgs_sw_long_reads(tmp_path, oracle, bgzf):
         got = np.fromfile(tmp_path / "scores" / (os.path.basename(f) + ".scores"), dtype=REC_T)
         assert np.array_equal(got["score"], s) and np.array_equal(got["end_i"], i) and np.array_equal(got["end_j"], j)
     rec = json.load(open(tmp_path / "rec.json"))
-    assert rec["total_score"] == want and rec["total_reads"] == 1400 and not rec["gpu_inflate"]
+    assert rec["total_score"] == want and rec["total_reads"] == 1400 and rec["gpu_inflate"] == bgzf
 
 
 @pytest.mark.gpu

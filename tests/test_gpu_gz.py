@@ -189,7 +189,7 @@ def gpu_reads(ctx, path, stride=256, max_reads=3000, span=1 << 20):
 
 
 def assert_reader_parity(ctx, path, **kw):
-    hs, hl, hp, hst = host_reads(path)
+    hs, hl, hp, hst = host_reads(path, kw.get("stride", 256))
     gs, gl, gp, gst = gpu_reads(ctx, path, **kw)
     assert len(hl) == len(gl)
     assert np.array_equal(hl, gl)
@@ -288,3 +288,20 @@ def test_inflate_truncated_deflate_stream(gpu_ctx, cut):
     blob = member + bgzf_compress(fastq_text(40, 22), 6)  # another member follows
     with pytest.raises(MswError, match="truncated deflate data"):
         bgzf_inflate(gpu_ctx, blob)
+
+
+
+@pytest.mark.parametrize("stride,lo,hi", [(512, 200, 512), (5008, 1, 5000)])
+def test_reader_wide_slabs(gpu_ctx, tmp_path, stride, lo, hi):
+    """Slab rows wider than 256 bytes (long reads, MSW_MAX_READ_LEN): the
+    emit pass writes each row 256 bytes per pass of the read's 16 lanes;
+    same reads, lengths and pos= as the host reader at that stride."""
+    rng = np.random.default_rng(stride)
+    recs = []
+    for i in range(1500):
+        m = int(rng.integers(lo, hi + 1))
+        seq = bytes(np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, m)])
+        recs.append(b"@r%d pos=%d\n" % (i, int(rng.integers(0, 10 ** 9))) + seq + b"\n+\n" + b"I" * m + b"\n")
+    p = tmp_path / "wide.fastq.gz"
+    p.write_bytes(bgzf_compress(b"".join(recs), 6, block=20000))
+    assert assert_reader_parity(gpu_ctx, str(p), stride=stride, max_reads=700) == 1500
