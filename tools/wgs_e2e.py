@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--qual", default="I", choices=["I", "binned", "illumina"], help="quality strings")
     ap.add_argument("--level", type=int, default=1, help="gzip compression level of the lane files")
     ap.add_argument("--num-gpus", type=int, default=1)
+    ap.add_argument("--read-len", type=int, default=150, help="read length (window = --window or 2x)")
+    ap.add_argument("--window", type=int, default=300)
     ap.add_argument("--reuse", action="store_true", help="keep an existing dataset in --dir")
     args = ap.parse_args()
 
@@ -54,7 +56,7 @@ def main():
         ds = write_wgs_dataset(args.dir, lanes=args.lanes, reads_per_lane=args.reads_per_lane,
                                reads_per_file=args.reads_per_file, genome_bases=args.genome_bases,
                                keep_batches=False, workers=args.workers, bgzf=args.bgzf, qual=args.qual,
-                               compresslevel=args.level)
+                               compresslevel=args.level, read_len=args.read_len)
     gen_s = time.time() - t0
     gz_bytes = sum(os.path.getsize(f) for f in ds["files"])
     print(f"dataset: {len(ds['files'])} files, {gz_bytes / 1e6:.0f} MB gz, written in {gen_s:.1f} s", flush=True)
@@ -68,6 +70,8 @@ def main():
         env = dict(os.environ, WGS_DATA_DIR=args.dir, WGS_SAMPLE_ID="SYN", WGS_LANES=str(args.lanes),
                    WGS_READS_PER_LANE=str(args.reads_per_lane), GPU_CHUNK_SIZE_READS=str(args.chunk),
                    WGS_RUN_ID=f"e2e_{kind}_{readers}_v{vi}_{int(time.time() * 1000)}")
+        if args.read_len > 256:
+            env["MSW_MAX_READ_LEN"] = str(args.read_len + 16)  # room for the synthetic indels
         if kind == "threads":
             env["MSW_HOST_THREADS"] = str(readers)
             env.pop("MSW_READERS", None)
@@ -78,7 +82,7 @@ def main():
             env[k] = v
         ts = time.time()
         r = subprocess.run([cli, "--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"],
-                            "--window", "300", "--checkpoint-dir", args.dir, "--json", rec,
+                            "--window", str(args.window), "--checkpoint-dir", args.dir, "--json", rec,
                             "--num-gpus", str(args.num_gpus)],
                            env=env, capture_output=True, text=True, timeout=900)
         wall = time.time() - ts
@@ -92,7 +96,7 @@ def main():
                   "chunk_reads": args.chunk, "extra_env": extra_env, "bgzf": args.bgzf, "qual": args.qual,
                   "level": args.level,
                   "dataset": f"{args.lanes} lanes x {args.reads_per_lane} files x {args.reads_per_file} "
-                             f"150 bp reads, {args.genome_bases} bp genome, window 300"})
+                             f"{args.read_len} bp reads, {args.genome_bases} bp genome, window {args.window}"})
         print(json.dumps(d), flush=True)
         with open(args.out, "a") as f:
             f.write(json.dumps(d) + "\n")
