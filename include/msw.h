@@ -21,7 +21,7 @@
  *    window) of the best cell, smallest i then smallest j on ties; (-1,-1)
  *    when the score is 0 or the pair is empty.
  *  - Supported by the GPU kernels: read and window lengths <= 32767 (pairs
- *    up to 256 x 4096 run on the packed 16-bit kernels, longer ones on the
+ *    up to 384 x 4096 run on the packed 16-bit kernels, longer ones on the
  *    i32 long-pair kernel, in the same call), 1 <= match <= 64,
  *    match - 64 <= mismatch <= 0, 0 <= gap_extend <= 1024,
  *    0 <= gap_open <= 30000.  Anything else -> MSW_E_RANGE.

@@ -124,7 +124,8 @@ hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_r
         return launch_split(p, affine, coords, kr, stream);
     }
     const int kr = rows_per_lane(max_read_len, false, p.group_lanes);
-    if (kr < 1 || kr > 16) return hipErrorInvalidValue;
+    if (kr < 1 || kr > kMaxRowsPerLane) return hipErrorInvalidValue;
+    if (kr > 16) return launch_pairs_wide(p, affine, coords, kr, stream);
     return affine ? launch_pairs_aff(p, coords, kr, stream) : launch_pairs_lin(p, coords, kr, stream);
 }
 

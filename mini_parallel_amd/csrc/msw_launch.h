@@ -10,6 +10,8 @@ namespace msw {
 // pairs layout, KR = 1..16 (msw_launch_pairs_lin.hip / msw_launch_pairs_aff.hip)
 hipError_t launch_pairs_lin(const SwParams& p, bool coords, int kr, hipStream_t stream);
 hipError_t launch_pairs_aff(const SwParams& p, bool coords, int kr, hipStream_t stream);
+// pairs layout, KR = 17..24 (G = 16: reads of 257..384 bases; msw_launch_pairs_wide.hip)
+hipError_t launch_pairs_wide(const SwParams& p, bool affine, bool coords, int kr, hipStream_t stream);
 // split layout, KR = 1..8 (msw_launch_split.hip)
 hipError_t launch_split(const SwParams& p, bool affine, bool coords, int kr, hipStream_t stream);
 // mixed grid, even KRP = 2..16 (msw_launch_mixed.hip)

@@ -452,7 +452,8 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
         for (uint32_t G = 16; G >= 8; --G) {
             if (force_g ? G != force_g : ((force_pairs || force_split) && G != 16)) continue;
             const int kr = msw::rows_per_lane(max_m, split, G);
-            if (kr > (split ? 8 : 16)) continue;
+            // KR 17..24 (reads of 257..384 bases) only in 16-lane groups
+            if (kr > (split ? 8 : (G == 16 ? msw::kMaxRowsPerLane : 16))) continue;
             const uint32_t groups = 64 / G;
             if (G != 16 && msw::lds_bytes(stride, groups) > 65536) continue;
             const uint64_t per = msw::pairs_per_wave(split, groups);
@@ -465,7 +466,7 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
     }
     // Mixed grid (G = 16, even KR): up to one pairs-wave per SIMD, then split waves.
     const int krp = msw::rows_per_lane(max_m, false);
-    const bool mixed_ok = (krp % 2) == 0 && (!force_g || force_g == 16) && !force_pairs && !force_split;
+    const bool mixed_ok = (krp % 2) == 0 && krp <= 16 && (!force_g || force_g == 16) && !force_pairs && !force_split;
     if (mixed_ok) {
         const double cp = wave_instr(false, 16), cs = wave_instr(true, 16);
         for (uint64_t k = 1; k <= 4; ++k) {
@@ -496,9 +497,9 @@ struct Bucket {
 void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32_t* order,
                   std::vector<Bucket>& buckets) {
     buckets.clear();
-    // key = KR (1..16) * 257 + ceil(n / 16) (<= 256): counting sort; pairs
+    // key = KR (1..24) * 257 + ceil(n / 16) (<= 256): counting sort; pairs
     // beyond the packed kernels' limits share the last key.
-    constexpr int kLongKey = 17 * 257, kKeys = kLongKey + 1;
+    constexpr int kLongKey = (msw::kMaxRowsPerLane + 1) * 257, kKeys = kLongKey + 1;
     std::vector<uint32_t> hist(kKeys + 1, 0);
     const bool all_long = force_long();
     auto key_of = [&](uint64_t i) {
@@ -528,7 +529,7 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
     std::vector<uint32_t> pos(hist.begin(), hist.end() - 1);
     for (uint64_t i = 0; i < n; ++i) order[pos[key_of(i)]++] = (uint32_t)i;
     // One bucket per KR value; the window bound is the bucket's max.
-    for (int kr = 1; kr <= 16; ++kr) {
+    for (int kr = 1; kr <= msw::kMaxRowsPerLane; ++kr) {
         const uint32_t b = hist[kr * 257], e = hist[kr * 257 + 257];
         if (e <= b) continue;
         uint32_t mm = 0, mn = 0;
@@ -554,10 +555,19 @@ size_t short_buckets(const std::vector<Bucket>& buckets) {
     return !buckets.empty() && buckets.back().long_pairs ? buckets.size() - 1 : buckets.size();
 }
 
+// The leading buckets sw_multi_kernel takes (KR <= 16; buckets come in KR
+// order); the rest of the packed buckets (KR 17..24) launch on their own.
+size_t multi_buckets(const std::vector<Bucket>& buckets) {
+    const size_t n = short_buckets(buckets);
+    size_t k = 0;
+    while (k < n && msw::rows_per_lane(buckets[k].max_m, false) <= msw::kMaxMultiKR) ++k;
+    return k;
+}
+
 // One-launch table of a bucket list (msw::MultiTable): heaviest waves first
 // (rows per lane x window steps), so the tail of the grid is short waves.
 void fill_multi(const std::vector<Bucket>& buckets, const Scheme& sch, msw::MultiTable& t) {
-    std::vector<Bucket> bs(buckets.begin(), buckets.begin() + short_buckets(buckets));
+    std::vector<Bucket> bs(buckets.begin(), buckets.begin() + multi_buckets(buckets));
     auto cost = [](const Bucket& b) { return (uint64_t)msw::rows_per_lane(b.max_m, false) * (b.max_n + 16u); };
     std::stable_sort(bs.begin(), bs.end(), [&](const Bucket& a, const Bucket& b) { return cost(a) > cost(b); });
     memset(&t, 0, sizeof(t));
@@ -604,7 +614,9 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         if (rc) return rc;
         if (n_short == 0) return MSW_OK;
     }
-    if (use_order && use_multi(n_short)) {
+    const size_t n_multi = multi_buckets(buckets);
+    size_t first_single = 0;
+    if (use_order && use_multi(n_multi)) {
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
         p.wins = s.d_wins;
@@ -624,9 +636,9 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         msw::MultiTable t;
         fill_multi(buckets, sch, t);
         HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
-        return MSW_OK;
+        first_single = n_multi;  // the KR 17..24 buckets follow on their own
     }
-    for (size_t bi = 0; bi < n_short; ++bi) {
+    for (size_t bi = first_single; bi < n_short; ++bi) {
         const Bucket& b = buckets[bi];
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
@@ -1190,8 +1202,9 @@ struct msw_plan {
     uint32_t* d_slot_lens = nullptr;  // read_len | win_len << 16 in slot order
     bool multi = false;
     msw::MultiTable table{};
-    LaunchPlan single{};
-    Bucket shorts{};                  // single (non-multi) launch: the one packed-kernel bucket
+    // packed-kernel buckets launched on their own (all of them without a
+    // multi table, else the KR 17..24 ones), each with its layout
+    std::vector<std::pair<Bucket, LaunchPlan>> singles;
     bool has_long = false;
     Bucket longs{};                   // pairs beyond the packed kernels (sw_long_kernel)
 };
@@ -1230,13 +1243,12 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
             pl->has_long = true;
             pl->longs = buckets.back();
         }
-        pl->multi = use_multi(n_short);
-        if (pl->multi) {
-            fill_multi(buckets, sch, pl->table);
-        } else if (n_short == 1) {
-            pl->shorts = buckets[0];
-            pl->single = choose_layout(pl->shorts.count, pl->shorts.max_m, pl->shorts.max_n, sch, ctx->cu_count);
-        }
+        const size_t n_multi = multi_buckets(buckets);
+        pl->multi = use_multi(n_multi);
+        if (pl->multi) fill_multi(buckets, sch, pl->table);
+        for (size_t bi = pl->multi ? n_multi : 0; bi < n_short; ++bi)
+            pl->singles.push_back({buckets[bi], choose_layout(buckets[bi].count, buckets[bi].max_m, buckets[bi].max_n,
+                                                              sch, ctx->cu_count)});
         rc = grow_dev(&pl->d_order, n_pairs);
         hipError_t e = rc ? hipSuccess : hipMemcpy(pl->d_order, order.data(), n_pairs * sizeof(uint32_t),
                                                    hipMemcpyHostToDevice);
@@ -1312,18 +1324,23 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
         if ((rc = launch_long(sch, q, plan->longs.count, plan->longs.max_m, plan->longs.max_n, st))) return rc;
     }
     if (plan->multi) {
-        p.group_lanes = 16;
-        p.groups = 4;
-        HIP_TRY(msw::launch_sw_multi(p, plan->table, sch.affine, sch.coords, st));
-    } else if (plan->shorts.count) {  // one packed-kernel bucket: slots [0, count)
-        const Bucket& b = plan->shorts;
-        p.n_slots = b.count;
-        p.lds_stride = msw::stream_stride(b.max_n);
-        p.f16_ok = f16_fits(sch, b.max_m, b.max_n) ? 1u : 0u;
-        p.pairs_blocks = plan->single.pairs_blocks;
-        p.group_lanes = plan->single.group_lanes;
-        p.groups = plan->single.groups;
-        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan->single.layout, st));
+        msw::SwParams q = p;
+        q.group_lanes = 16;
+        q.groups = 4;
+        HIP_TRY(msw::launch_sw_multi(q, plan->table, sch.affine, sch.coords, st));
+    }
+    for (const auto& sb : plan->singles) {  // slots [b.begin, b.begin + count)
+        const Bucket& b = sb.first;
+        msw::SwParams q = p;
+        q.order = plan->d_order + b.begin;
+        q.out_slot_base = b.begin;
+        q.n_slots = b.count;
+        q.lds_stride = msw::stream_stride(b.max_n);
+        q.f16_ok = f16_fits(sch, b.max_m, b.max_n) ? 1u : 0u;
+        q.pairs_blocks = sb.second.pairs_blocks;
+        q.group_lanes = sb.second.group_lanes;
+        q.groups = sb.second.groups;
+        HIP_TRY(msw::launch_sw(q, sch.affine, sch.coords, b.max_m, sb.second.layout, st));
     }
     if (!plan->identity)
         HIP_TRY(msw::launch_gather_results(plan->d_inv, t_score, t_i, t_j, out->score, sch.coords ? out->end_i : nullptr,
