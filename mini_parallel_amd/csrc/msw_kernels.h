@@ -78,6 +78,10 @@ struct SwParams {
     // long_cols i32 columns each (x2 for affine: H then F).
     int32_t* long_scratch;
     uint32_t long_cols;
+    // sw_long_kernel work queue (zeroed u32, or null): with fewer blocks than
+    // slots, a block that finishes a slot takes the next unclaimed one
+    // (gridDim.x + counter) instead of striding by gridDim.x
+    uint32_t* long_next;
 };
 
 // f16 bits of the cell value v * 2^-11 (|v| < 2048: exact, normal or zero).
@@ -162,6 +166,9 @@ hipError_t launch_gather_results(const uint32_t* inv, const int32_t* src_score, 
 // <= 512 rows, rows spread evenly over them); scratch columns per block; LDS bytes.
 int long_rows_per_lane(uint32_t max_read_len);
 uint32_t long_scratch_cols(uint32_t max_win_len);
+// Blocks (waves) of the long-pair launch one CU holds at once (registers and
+// LDS of the kernel instance these bounds select).
+int long_blocks_per_cu(bool affine, bool coords, uint32_t max_read_len, uint32_t max_win_len);
 size_t long_lds_bytes(uint32_t max_win_len);
 // One wave per pair, `blocks` blocks striding over p.n_slots (order / slot
 // results as in launch_sw).  p.long_scratch must hold blocks x long_cols

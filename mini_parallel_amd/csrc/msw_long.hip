@@ -9,7 +9,9 @@
 // with the same conventions as the oracle (oracle/sw_oracle.c): i32 cells,
 // best cell = max score, then smallest i, then smallest j.
 //
-// Mapping (one wave64 per pair; blocks loop over the launch's slots):
+// Mapping (one wave64 per pair; blocks take the launch's slots from a work
+// queue, heaviest first when the host sorted them -- msw_runtime.cpp
+// bucket_chunk -- so mixed lengths balance over the SIMDs):
 //  * the read is cut into strips of 64*R rows (R = 1..8 rows per lane); in a
 //    strip, lane l owns rows [l*R, l*R+R) and sweeps the window with the
 //    one-column-per-lane skew of the packed kernels: at step t it scores
@@ -74,7 +76,14 @@ __global__ __launch_bounds__(64) void sw_long_kernel(SwParams p) {
     int32_t* const bnd_h = p.long_scratch ? p.long_scratch + (size_t)blockIdx.x * cols * (AFFINE ? 2u : 1u) : nullptr;
     int32_t* const bnd_f = bnd_h ? bnd_h + cols : nullptr;
 
-    for (uint32_t slot = blockIdx.x; slot < p.n_slots; slot += gridDim.x) {
+    // next slot: one atomic per slot from lane 0 when the queue is on
+    auto next_slot = [&](uint32_t slot) {
+        if (!p.long_next) return slot + gridDim.x;
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(p.long_next, 1u);
+        return gridDim.x + (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+    };
+    for (uint32_t slot = blockIdx.x; slot < p.n_slots; slot = next_slot(slot)) {
         const uint32_t pair = p.order ? p.order[slot] : p.slot_base + slot;
         const uint32_t outi = p.out_by_slot ? p.out_slot_base + slot : pair;
         const int m = p.read_len[pair], n = p.win_len[pair];
@@ -241,7 +250,34 @@ hipError_t go(const SwParams& p, bool affine, bool coords, uint32_t blocks, size
     return hipGetLastError();
 }
 
+template <int R>
+int resident(bool affine, bool coords, size_t shm) {
+    int nb = 0;
+    hipError_t e;
+    if (affine)
+        e = coords ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_long_kernel<R, true, true>, 64, shm)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_long_kernel<R, true, false>, 64, shm);
+    else
+        e = coords ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_long_kernel<R, false, true>, 64, shm)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_long_kernel<R, false, false>, 64, shm);
+    return e == hipSuccess && nb > 0 ? nb : 1;
+}
+
 }  // namespace
+
+int long_blocks_per_cu(bool affine, bool coords, uint32_t max_read_len, uint32_t max_win_len) {
+    const size_t shm = long_lds_bytes(max_win_len);
+    switch (long_rows_per_lane(max_read_len)) {
+        case 1: return resident<1>(affine, coords, shm);
+        case 2: return resident<2>(affine, coords, shm);
+        case 3: return resident<3>(affine, coords, shm);
+        case 4: return resident<4>(affine, coords, shm);
+        case 5: return resident<5>(affine, coords, shm);
+        case 6: return resident<6>(affine, coords, shm);
+        case 7: return resident<7>(affine, coords, shm);
+        default: return resident<8>(affine, coords, shm);
+    }
+}
 
 int long_rows_per_lane(uint32_t max_read_len) {
     // as few strips of <= 64 * kLongMaxR rows as the longest read needs, its

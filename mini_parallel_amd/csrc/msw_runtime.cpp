@@ -150,23 +150,47 @@ inline bool force_long() {
 }
 
 // Long-pair launch (p's pointers, order and output fields set by the caller):
-// one wave per pair, blocks striding over the pairs: up to 16 waves per SIMD
-// when one strip holds every read, 8 when reads need per-block boundary rows
-// (allocated stream-ordered on `st`, so calls on any stream stay independent).
-int launch_long(const Scheme& sch, msw::SwParams p, uint64_t n, uint32_t max_m, uint32_t max_n, hipStream_t st) {
+// one wave per pair, one block per slot: the dispatcher fills every wave slot
+// the kernel's registers and LDS allow and refills freed ones in slot order,
+// so with the slots of spread lengths sorted heaviest first (`spread`,
+// bucket_chunk) that is longest-job-first over the SIMDs (tools/long_bench.py
+// mixed 257-2000: 2.4 -> 3.9 TCUPS).  Equal pairs whose last round would be a
+// short tail (<= 1/8 of the resident waves, running almost alone) are spread
+// evenly over the fewest rounds instead (150 x 5000: 3.0 -> 3.6 TCUPS; with
+// larger tails keeping full occupancy measured faster).  Past a block cap
+// (boundary-row scratch <= 1 GiB), finished blocks take the next slot from a
+// work queue.  Scratch and queue counter are allocated stream-ordered on
+// `st`, so calls on any stream stay independent.
+int launch_long(const Scheme& sch, msw::SwParams p, uint64_t n, uint32_t max_m, uint32_t max_n, bool spread,
+                int cu_count, hipStream_t st) {
     if (n == 0) return MSW_OK;
     p.n_slots = (uint32_t)n;
     const bool strips = max_m > 64u * (uint32_t)msw::long_rows_per_lane(max_m);
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(n, strips ? 8192 : 16384);
-    int32_t* scratch = nullptr;
-    if (strips) {
-        p.long_cols = msw::long_scratch_cols(max_n);
-        HIP_TRY(hipMallocAsync((void**)&scratch,
-                               (size_t)blocks * p.long_cols * (sch.affine ? 2u : 1u) * sizeof(int32_t), st));
+    const size_t per_block = strips ? (size_t)msw::long_scratch_cols(max_n) * (sch.affine ? 2u : 1u) * sizeof(int32_t) : 0;
+    const uint64_t resident =
+        (uint64_t)(cu_count > 0 ? cu_count : 256) * (uint64_t)msw::long_blocks_per_cu(sch.affine, sch.coords, max_m, max_n);
+    uint64_t blocks = n;
+    if (!spread && n > resident && n % resident != 0 && (n % resident) * 8 <= resident) {
+        const uint64_t rounds = (n + resident - 1) / resident;
+        blocks = (n + rounds - 1) / rounds;
     }
-    p.long_scratch = scratch;
-    const hipError_t e = msw::launch_sw_long(p, sch.affine, sch.coords, max_m, max_n, blocks, st);
-    if (scratch) HIP_TRY(hipFreeAsync(scratch, st));
+    blocks = std::min<uint64_t>(blocks, per_block ? std::max<uint64_t>(resident, (1ull << 30) / per_block) : 1ull << 20);
+    const char* env = getenv("MSW_LONG_BLOCKS");  // experiments: a fixed block count
+    if (env && atoll(env) > 0) blocks = std::min<uint64_t>(n, (uint64_t)atoll(env));
+    const bool queue = n > blocks;
+    const size_t scratch_bytes = (size_t)blocks * per_block;
+    uint8_t* mem = nullptr;
+    if (strips || queue) {
+        HIP_TRY(hipMallocAsync((void**)&mem, scratch_bytes + 256, st));
+        p.long_scratch = strips ? reinterpret_cast<int32_t*>(mem) : nullptr;
+        p.long_cols = strips ? msw::long_scratch_cols(max_n) : 0u;
+        if (queue) {
+            p.long_next = reinterpret_cast<uint32_t*>(mem + scratch_bytes);
+            HIP_TRY(hipMemsetAsync(p.long_next, 0, sizeof(uint32_t), st));
+        }
+    }
+    const hipError_t e = msw::launch_sw_long(p, sch.affine, sch.coords, max_m, max_n, (uint32_t)blocks, st);
+    if (mem) HIP_TRY(hipFreeAsync(mem, st));
     HIP_TRY(e);
     return MSW_OK;
 }
@@ -244,6 +268,7 @@ struct msw_ctx {
     int device = 0;
     int cu_count = 256;
     hipStream_t compute = nullptr, copy = nullptr, d2h = nullptr;
+    hipStream_t side = nullptr;  // long-pair launches beside packed ones (fork_side)
     // Staging slots, used round robin by successive chunks (and calls): with
     // three, the host stages chunk k+1 while k runs and k-1 drains, so the
     // uploads of k+1 finish under kernel k.
@@ -492,6 +517,7 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
 struct Bucket {
     uint32_t begin, count, max_m, max_n;
     bool long_pairs = false;  // beyond the packed kernels: sw_long_kernel
+    bool spread = false;      // long pairs of spread lengths, sorted heaviest first
 };
 
 void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32_t* order,
@@ -509,17 +535,21 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
         return kr * 257 + nb;
     };
     // One key (fixed-length reads and windows, the common case): one bucket in
-    // input order, no sort.
+    // input order, no sort -- unless they are long pairs of spread lengths,
+    // which the work queue wants heaviest first.
     int kmin = kKeys, kmax = -1;
-    uint32_t gm = 0, gn = 0;
+    uint32_t gm = 0, gn = 0, lm = 0xFFFF, ln = 0xFFFF;
     for (uint64_t i = 0; i < n; ++i) {
         const int k = key_of(i);
         kmin = std::min(kmin, k);
         kmax = std::max(kmax, k);
         gm = std::max<uint32_t>(gm, rlen[i]);
         gn = std::max<uint32_t>(gn, wlen[i]);
+        lm = std::min<uint32_t>(lm, rlen[i]);
+        ln = std::min<uint32_t>(ln, wlen[i]);
     }
-    if (n && kmin == kmax) {
+    const bool spread_long = kmin == kLongKey && (gm - lm >= 64 || gn - ln >= 64);
+    if (n && kmin == kmax && !spread_long) {
         for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
         buckets.push_back({0, (uint32_t)n, gm, gn, kmin == kLongKey});
         return;
@@ -546,7 +576,14 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
             mm = std::max<uint32_t>(mm, rlen[order[s]]);
             mn = std::max<uint32_t>(mn, wlen[order[s]]);
         }
-        buckets.push_back({b, e - b, mm, mn, true});
+        // heaviest first (strips x steps at the launch's rows per lane): the
+        // kernel's work queue then schedules longest-job-first
+        const uint32_t strip_rows = 64u * (uint32_t)msw::long_rows_per_lane(mm);
+        auto cost = [&](uint32_t i) {
+            return (uint64_t)((rlen[i] + strip_rows - 1) / strip_rows) * (uint64_t)(wlen[i] + 63u);
+        };
+        std::stable_sort(order + b, order + e, [&](uint32_t x, uint32_t y) { return cost(x) > cost(y); });
+        buckets.push_back({b, e - b, mm, mn, true, cost(order[b]) != cost(order[e - 1])});
     }
 }
 
@@ -591,10 +628,38 @@ bool use_multi(size_t n_buckets) {
     return n_buckets > 1 && !getenv("MSW_NO_MULTI") && !getenv("MSW_LAYOUT") && !getenv("MSW_GROUP_LANES");
 }
 
+// A long-pair launch next to packed launches runs on the context's side
+// stream, forked from `st` and joined back after the packed launches: the
+// long kernel's tail and the packed buckets' short launches (a few lone waves
+// each for KR 17..24) share the CUs instead of queueing behind each other.
+struct SideFork {
+    hipEvent_t ev = nullptr;
+    SideFork() = default;
+    SideFork(const SideFork&) = delete;
+    SideFork& operator=(const SideFork&) = delete;
+    ~SideFork() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+
+int fork_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
+    HIP_TRY(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(f.ev, st));
+    HIP_TRY(hipStreamWaitEvent(ctx->side, f.ev, 0));
+    return MSW_OK;
+}
+
+int join_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
+    HIP_TRY(hipEventRecord(f.ev, ctx->side));
+    HIP_TRY(hipStreamWaitEvent(st, f.ev, 0));
+    return MSW_OK;
+}
+
 int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const std::vector<Bucket>& buckets,
                    bool use_order, uint32_t read_stride, uint32_t win_stride) {
     const size_t n_short = short_buckets(buckets);
-    if (n_short < buckets.size()) {  // long pairs: their own launch on the same stream
+    SideFork side;
+    if (n_short < buckets.size()) {  // long pairs: their own launch, beside any packed ones
         const Bucket& b = buckets.back();
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
@@ -610,7 +675,10 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.end_j = sch.coords ? s.d_ej : nullptr;
         p.read_stride = read_stride;
         p.win_stride = win_stride;
-        int rc = launch_long(sch, p, b.count, b.max_m, b.max_n, ctx->compute);
+        int rc = n_short ? fork_side(ctx, ctx->compute, side) : MSW_OK;
+        if (!rc)
+            rc = launch_long(sch, p, b.count, b.max_m, b.max_n, use_order && b.spread, ctx->cu_count,
+                             n_short ? ctx->side : ctx->compute);
         if (rc) return rc;
         if (n_short == 0) return MSW_OK;
     }
@@ -663,6 +731,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.groups = plan.groups;
         HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan.layout, ctx->compute));
     }
+    if (side.ev) return join_side(ctx, ctx->compute, side);
     (void)n;
     return MSW_OK;
 }
@@ -857,6 +926,12 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
                 mx = std::max<uint32_t>(mx, s.h_wlen[i]);
             }
             uniform = (mx - mn) < 16;
+            // long pairs of spread read lengths keep their heaviest-first order
+            if (buckets[0].long_pairs) {
+                uint32_t lo = 0xFFFF;
+                for (uint64_t i = 0; i < cnt; ++i) lo = std::min<uint32_t>(lo, s.h_rlen[i]);
+                uniform = uniform && buckets[0].max_m - lo < 64;
+            }
         }
         if (tr.on) tr.stage += tr.lap();
         // H2D on the copy stream, kernels on the compute stream (a one-chunk
@@ -950,6 +1025,7 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
         (void)hipStreamSynchronize(ctx->copy);
         (void)hipStreamSynchronize(ctx->compute);
         (void)hipStreamSynchronize(ctx->d2h);
+        (void)hipStreamSynchronize(ctx->side);
         for (Slot& s : ctx->slots)
             if (s.busy && s.ticket == ticket) s.busy = false;
         ctx->next_ticket++;
@@ -1043,6 +1119,7 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         return fail(MSW_E_DEVICE, "context creation on device %d failed: %s", ordinal, hipGetErrorString(e));
@@ -1057,6 +1134,7 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     if (ctx->compute) (void)hipStreamSynchronize(ctx->compute);
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
     if (ctx->d2h) (void)hipStreamSynchronize(ctx->d2h);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
     for (Slot& s : ctx->slots) {
         if (s.uploaded) (void)hipEventDestroy(s.uploaded);
         if (s.computed) (void)hipEventDestroy(s.computed);
@@ -1081,6 +1159,7 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     delete ctx;
 }
 
@@ -1169,7 +1248,7 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
     // bounds past the packed kernels: the whole batch on the long-pair kernel
     if (force_long() || is_long(max_read_len, max_win_len))
-        return launch_long(sch, p, b->n_pairs, max_read_len, max_win_len, st);
+        return launch_long(sch, p, b->n_pairs, max_read_len, max_win_len, false, ctx->cu_count, st);
     p.lds_stride = msw::stream_stride(max_win_len);
     p.win_vec = msw::vec_ok(p.wins, p.win_stride);
     p.f16_ok = f16_fits(sch, max_read_len, max_win_len) ? 1u : 0u;
@@ -1316,12 +1395,17 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
         p.end_i = sch.coords ? t_i : nullptr;
         p.end_j = sch.coords ? t_j : nullptr;
     }
+    SideFork side;
     if (plan->has_long) {  // the long pairs' slots come last: [longs.begin, n)
         msw::SwParams q = p;
         q.order = plan->d_order + plan->longs.begin;
         q.out_slot_base = plan->longs.begin;
         q.slot_lens = nullptr;
-        if ((rc = launch_long(sch, q, plan->longs.count, plan->longs.max_m, plan->longs.max_n, st))) return rc;
+        const bool beside = plan->multi || !plan->singles.empty();
+        if (beside && (rc = fork_side(ctx, st, side))) return rc;
+        if ((rc = launch_long(sch, q, plan->longs.count, plan->longs.max_m, plan->longs.max_n, plan->longs.spread,
+                              ctx->cu_count, beside ? ctx->side : st)))
+            return rc;
     }
     if (plan->multi) {
         msw::SwParams q = p;
@@ -1342,6 +1426,7 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
         q.groups = sb.second.groups;
         HIP_TRY(msw::launch_sw(q, sch.affine, sch.coords, b.max_m, sb.second.layout, st));
     }
+    if (side.ev && (rc = join_side(ctx, st, side))) return rc;
     if (!plan->identity)
         HIP_TRY(msw::launch_gather_results(plan->d_inv, t_score, t_i, t_j, out->score, sch.coords ? out->end_i : nullptr,
                                            sch.coords ? out->end_j : nullptr, n, st));

@@ -106,6 +106,40 @@ def test_long_random_batch(gpu_ctx, oracle, kind):
                 oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc), sc.want_coords)
 
 
+@pytest.mark.parametrize("blocks", ["1", "7", "0"])
+@pytest.mark.parametrize("kind", ["linear", "affine_coords"])
+def test_long_work_queue(gpu_ctx, oracle, monkeypatch, kind, blocks):
+    """Long pairs of spread lengths (sorted heaviest first by the host) with
+    fewer blocks than pairs (MSW_LONG_BLOCKS; "0" = the default grid): the
+    blocks take slots from the launch's work queue -- host batches, the device
+    API (input order) and a plan."""
+    import torch
+    monkeypatch.setenv("MSW_LONG_BLOCKS", blocks)
+    sc = scoring(kind)
+    b = make_pairs(90, (257, 1300), seed=77)
+    want = oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc)
+    assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc), want, sc.want_coords)
+    n = b.n_pairs
+    dR, dW, drl, dwl = _device([b.reads, b.wins, b.read_len.view(np.int16), b.win_len.view(np.int16)])
+    score, ei, ej = _device([np.zeros(n, np.int32), np.zeros(n, np.int16), np.zeros(n, np.int16)])
+    gpu_ctx.align_batch_device(dR.data_ptr(), drl.data_ptr(), dW.data_ptr(), dwl.data_ptr(), b.reads.shape[1],
+                               b.wins.shape[1], n, score.data_ptr(), int(b.read_len.max()), int(b.win_len.max()), sc,
+                               ei.data_ptr(), ej.data_ptr())
+    torch.cuda.synchronize()
+    gpu_ctx.synchronize()
+    assert_same((score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy()), want, sc.want_coords)
+    score.zero_()
+    launch = gpu_ctx.prepare_planned_launch(dR.data_ptr(), drl.data_ptr(), dW.data_ptr(), dwl.data_ptr(),
+                                            b.reads.shape[1], b.wins.shape[1], b.read_len, b.win_len,
+                                            score.data_ptr(), sc, ei.data_ptr(), ej.data_ptr())
+    try:
+        launch()
+        gpu_ctx.synchronize()
+        assert_same((score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy()), want, sc.want_coords)
+    finally:
+        launch.close()
+
+
 @pytest.mark.parametrize("chunk", [0, 37, 500])
 @pytest.mark.parametrize("kind", ["linear", "affine_coords"])
 def test_long_mixed_with_short(gpu_ctx, oracle, kind, chunk):

@@ -17,6 +17,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="run the cases whose name contains this")
     args = ap.parse_args()
     import torch
     from mini_parallel_amd import Context, Scoring
@@ -27,8 +28,11 @@ def main():
     kinds = {"linear": Scoring(), "affine_coords": Scoring(affine=True, gap_open=3, gap_extend=1, want_coords=True)}
     cases = [("300x600", 40_000, 300, 2.0, False), ("1000x2000", 4_000, 1000, 2.0, False),
              ("150x5000", 8_000, 150, 5000 / 150, False), ("150x300_forced", 10_000, 150, 2.0, True),
-             ("150x300_packed", 10_000, 150, 2.0, False), ("mixed_257-2000x2", 8_000, (257, 2000), 2.0, False)]
+             ("150x300_packed", 10_000, 150, 2.0, False), ("mixed_257-2000x2", 8_000, (257, 2000), 2.0, False),
+             ("mixed_500-2000x2", 8_000, (500, 2000), 2.0, False)]
     for name, n, m, wf, force in cases:
+        if args.only not in name:
+            continue
         b = make_pairs(n, m, win_factor=wf, seed=4242)
         t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
              (b.reads, b.wins, b.read_len.view(np.int16), b.win_len.view(np.int16))]
