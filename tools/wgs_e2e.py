@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--level", type=int, default=1, help="gzip compression level of the lane files")
     ap.add_argument("--num-gpus", type=int, default=1)
     ap.add_argument("--read-len", type=int, default=150, help="read length (window = --window or 2x)")
+    ap.add_argument("--cli", default="", help="CLI binary (A/B against another build)")
     ap.add_argument("--window", type=int, default=300)
     ap.add_argument("--reuse", action="store_true", help="keep an existing dataset in --dir")
     args = ap.parse_args()
@@ -60,7 +61,7 @@ def main():
     gen_s = time.time() - t0
     gz_bytes = sum(os.path.getsize(f) for f in ds["files"])
     print(f"dataset: {len(ds['files'])} files, {gz_bytes / 1e6:.0f} MB gz, written in {gen_s:.1f} s", flush=True)
-    cli = os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini")
+    cli = args.cli or os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini")
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     sweep = ([("threads", int(x)) for x in args.host_threads.split(",")] if args.host_threads
              else [("readers", int(x)) for x in args.readers.split(",")])
