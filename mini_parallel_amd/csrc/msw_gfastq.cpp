@@ -31,6 +31,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../include/msw.h"
 #include "../../include/msw_fastq.h"
 #include "msw_gz.h"
@@ -359,17 +361,47 @@ void release(msw_gfastq* g) {
     delete g;
 }
 
-// Top up hc with compressed bytes from the file (up to cap).
+// Top up hc with compressed bytes from the file (up to want, within cap).
+// Positioned reads (pread at fread_off); a large top-up -- a new file's
+// first span, ~180 MB at the config-4 shape -- is split over 4 threads
+// (MSW_GZ_READ_THREADS, 1..8): one
+// thread copies page-cache data into pinned memory at ~11 GB/s, and 16 ms of
+// it per file left the GPU idle between files (MSW_GFASTQ_TRACE).
 int fill_compressed(msw_gfastq* g, size_t want) {
-    while (g->hc_len < want && g->fread_off < g->fsize) {
-        const size_t n = (size_t)std::min<uint64_t>(std::min<size_t>(kReadPiece, g->hc_cap - g->hc_len),
-                                                    g->fsize - g->fread_off);
-        if (n == 0) break;
-        const size_t got = fread(g->hc + g->hc_len, 1, n, g->f);
-        if (got != n) return set_error(MSW_E_INVALID, "Error reading %s: short read", g->path.c_str());
-        g->hc_len += got;
-        g->fread_off += got;
+    want = std::min(want, g->hc_cap);
+    if (want <= g->hc_len || g->fread_off >= g->fsize) return MSW_OK;
+    const uint64_t todo = std::min<uint64_t>(want - g->hc_len, g->fsize - g->fread_off);
+    const int fd = fileno(g->f);
+    auto piece = [fd](uint8_t* dst, uint64_t off, uint64_t len) {
+        while (len) {
+            const ssize_t r = pread(fd, dst, (size_t)std::min<uint64_t>(len, kReadPiece), (off_t)off);
+            if (r <= 0) return false;
+            dst += r;
+            off += (uint64_t)r;
+            len -= (uint64_t)r;
+        }
+        return true;
+    };
+    static const int threads = [] {
+        const char* e = getenv("MSW_GZ_READ_THREADS");
+        const int t = e ? atoi(e) : 4;
+        return t < 1 ? 1 : (t > 8 ? 8 : t);
+    }();
+    const int parts = todo >= (32u << 20) ? threads : 1;
+    const uint64_t per = (todo + parts - 1) / parts;
+    bool ok[8] = {true, true, true, true, true, true, true, true};
+    std::vector<std::thread> th;
+    for (int k = 1; k < parts; ++k) {
+        const uint64_t b = per * k, e = std::min<uint64_t>(todo, b + per);
+        if (b < e)
+            th.emplace_back([&, k, b, e]() { ok[k] = piece(g->hc + g->hc_len + b, g->fread_off + b, e - b); });
     }
+    ok[0] = piece(g->hc + g->hc_len, g->fread_off, std::min<uint64_t>(todo, per));
+    for (std::thread& t : th) t.join();
+    if (!std::all_of(ok, ok + 8, [](bool b) { return b; }))
+        return set_error(MSW_E_INVALID, "Error reading %s: short read", g->path.c_str());
+    g->hc_len += (size_t)todo;
+    g->fread_off += todo;
     return MSW_OK;
 }
 

@@ -453,14 +453,18 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
             const uint64_t k = (w + simds - 1) / simds;
             return (double)k * c * simd_cycles_per_instr(k);
         }
-        std::vector<double> load(simds, 0.0);
-        std::vector<uint32_t> cnt(simds, 0);
-        for (uint64_t i = 0; i < w; ++i) {
-            load[i % simds] += i < w1 ? c1 : c2;
-            cnt[i % simds]++;
-        }
+        // SIMD i holds w1 / S + (i < w1 % S) first-kind waves of w / S + (i <
+        // w % S): constant between the two breakpoints, so three SIMDs cover
+        // every case (closed form: a loop over the waves cost ~1 ms of host
+        // time per 2M-pair launch, stalling the GPU between kernels)
+        const uint64_t b1 = w1 % simds, b = w % simds;
         double t = 0.0;
-        for (uint64_t i = 0; i < simds; ++i) t = std::max(t, load[i] * simd_cycles_per_instr(cnt[i]));
+        for (uint64_t i : {(uint64_t)0, std::min(b1, b), std::max(b1, b)}) {
+            if (i >= simds) continue;
+            const uint64_t n1 = w1 / simds + (i < b1 ? 1 : 0), n = w / simds + (i < b ? 1 : 0);
+            if (n == 0) continue;
+            t = std::max(t, ((double)n1 * c1 + (double)(n - n1) * c2) * simd_cycles_per_instr(n));
+        }
         return t;
     };
     const uint32_t stride = msw::stream_stride(max_n);
