@@ -382,12 +382,12 @@ int fill_compressed(msw_gfastq* g, size_t want) {
         }
         return true;
     };
-    static const int threads = [] {
-        const char* e = getenv("MSW_GZ_READ_THREADS");
-        const int t = e ? atoi(e) : 4;
-        return t < 1 ? 1 : (t > 8 ? 8 : t);
-    }();
-    const int parts = todo >= (32u << 20) ? threads : 1;
+    // read per call (a few per file): tests change them between readers
+    const char* et = getenv("MSW_GZ_READ_THREADS");
+    const char* es = getenv("MSW_GZ_READ_SPLIT");  // smallest top-up split over threads (bytes)
+    const int threads = std::max(1, std::min(8, et ? atoi(et) : 4));
+    const uint64_t split = es && atoll(es) > 0 ? (uint64_t)atoll(es) : (32ull << 20);
+    const int parts = todo >= split ? threads : 1;
     const uint64_t per = (todo + parts - 1) / parts;
     bool ok[8] = {true, true, true, true, true, true, true, true};
     std::vector<std::thread> th;

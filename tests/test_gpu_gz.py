@@ -210,6 +210,19 @@ def test_reader_matches_host_reader(gpu_ctx, tmp_path, block, crlf):
     assert n == 20_000
 
 
+@pytest.mark.parametrize("threads", ["3", "8"])
+def test_reader_parallel_compressed_reads(gpu_ctx, tmp_path, monkeypatch, threads):
+    """Compressed top-ups split over several positioned-read threads
+    (MSW_GZ_READ_THREADS; MSW_GZ_READ_SPLIT lowers the 32 MiB threshold so a
+    small file takes the split path, with parts ending mid-member)."""
+    monkeypatch.setenv("MSW_GZ_READ_THREADS", threads)
+    monkeypatch.setenv("MSW_GZ_READ_SPLIT", "4099")
+    data = fastq_text(20_000, 23)
+    p = tmp_path / "lane.fastq.gz"
+    p.write_bytes(bgzf_compress(data, 6, block=0xFF00))
+    assert assert_reader_parity(gpu_ctx, str(p)) == 20_000
+
+
 def test_reader_edge_files(gpu_ctx, tmp_path):
     rng = np.random.default_rng(5)
     cases = {
