@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <thread>
 #include <vector>
@@ -393,8 +394,12 @@ int fill_compressed(msw_gfastq* g, size_t want) {
     std::vector<std::thread> th;
     for (int k = 1; k < parts; ++k) {
         const uint64_t b = per * k, e = std::min<uint64_t>(todo, b + per);
-        if (b < e)
+        if (b >= e) continue;
+        try {
             th.emplace_back([&, k, b, e]() { ok[k] = piece(g->hc + g->hc_len + b, g->fread_off + b, e - b); });
+        } catch (const std::exception&) {  // no thread to spare: read this part here
+            ok[k] = piece(g->hc + g->hc_len + b, g->fread_off + b, e - b);
+        }
     }
     ok[0] = piece(g->hc + g->hc_len, g->fread_off, std::min<uint64_t>(todo, per));
     for (std::thread& t : th) t.join();
