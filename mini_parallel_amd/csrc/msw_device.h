@@ -1179,7 +1179,10 @@ __device__ __forceinline__ void multi_body(const SwParams& q, uint32_t blk, uint
     trace_end(q, wc, fast, false, KR, t_loop);
 }
 
-template <bool AFFINE, bool COORDS>
+// WIDE: the table's buckets have 17..24 rows per lane (reads of 257..384
+// bases) -- a separate instance, so their registers do not lower the
+// occupancy of the common KR <= 16 instance.
+template <bool AFFINE, bool COORDS, bool WIDE = false>
 __global__ __launch_bounds__(64) void sw_multi_kernel(SwParams p, MultiTable t) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t b = 0;
@@ -1191,6 +1194,19 @@ __global__ __launch_bounds__(64) void sw_multi_kernel(SwParams p, MultiTable t) 
     q.n_slots = t.count[b];
     q.lds_stride = t.lds_stride[b];
     q.f16_ok = t.f16_ok[b];
+    if constexpr (WIDE) {
+        switch (t.kr[b]) {
+            case 17: multi_body<17, AFFINE, COORDS>(q, blk, lds); break;
+            case 18: multi_body<18, AFFINE, COORDS>(q, blk, lds); break;
+            case 19: multi_body<19, AFFINE, COORDS>(q, blk, lds); break;
+            case 20: multi_body<20, AFFINE, COORDS>(q, blk, lds); break;
+            case 21: multi_body<21, AFFINE, COORDS>(q, blk, lds); break;
+            case 22: multi_body<22, AFFINE, COORDS>(q, blk, lds); break;
+            case 23: multi_body<23, AFFINE, COORDS>(q, blk, lds); break;
+            default: multi_body<24, AFFINE, COORDS>(q, blk, lds); break;
+        }
+        return;
+    }
     switch (t.kr[b]) {
         case 1: multi_body<1, AFFINE, COORDS>(q, blk, lds); break;
         case 2: multi_body<2, AFFINE, COORDS>(q, blk, lds); break;

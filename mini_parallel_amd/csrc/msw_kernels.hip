@@ -134,13 +134,18 @@ hipError_t launch_sw_multi(const SwParams& p, const MultiTable& t, bool affine, 
     if (t.n_buckets == 0) return hipSuccess;
     if (!p.order || t.n_buckets > (uint32_t)kMaxBuckets || p.group_lanes != 16 || p.groups != 4)
         return hipErrorInvalidValue;
+    // one table is all KR <= 16 buckets or all KR 17..24 (the wide instance)
+    const bool wide = t.kr[0] > (uint32_t)kMaxMultiKR;
     uint32_t stride = 0;
     for (uint32_t b = 0; b < t.n_buckets; ++b) {
-        if (t.kr[b] < 1 || t.kr[b] > 16) return hipErrorInvalidValue;
+        const bool ok = wide ? t.kr[b] > (uint32_t)kMaxMultiKR && t.kr[b] <= (uint32_t)kMaxRowsPerLane
+                             : t.kr[b] >= 1 && t.kr[b] <= (uint32_t)kMaxMultiKR;
+        if (!ok) return hipErrorInvalidValue;
         stride = max(stride, t.lds_stride[b]);
     }
     const uint32_t grid = t.block_end[t.n_buckets - 1];
     const size_t shm = lds_bytes(stride, p.groups);
+    if (wide) return launch_multi_wide(p, t, affine, coords, grid, shm, stream);
     return affine ? launch_multi_aff(p, t, coords, grid, shm, stream) : launch_multi_lin(p, t, coords, grid, shm, stream);
 }
 

@@ -21,5 +21,8 @@ hipError_t launch_multi_lin(const SwParams& p, const MultiTable& t, bool coords,
                             hipStream_t stream);
 hipError_t launch_multi_aff(const SwParams& p, const MultiTable& t, bool coords, uint32_t grid, size_t shm,
                             hipStream_t stream);
+// the same over KR 17..24 buckets (msw_launch_multi_wide.hip)
+hipError_t launch_multi_wide(const SwParams& p, const MultiTable& t, bool affine, bool coords, uint32_t grid,
+                             size_t shm, hipStream_t stream);
 
 }  // namespace msw

@@ -607,8 +607,10 @@ size_t multi_buckets(const std::vector<Bucket>& buckets) {
 
 // One-launch table of a bucket list (msw::MultiTable): heaviest waves first
 // (rows per lane x window steps), so the tail of the grid is short waves.
-void fill_multi(const std::vector<Bucket>& buckets, const Scheme& sch, msw::MultiTable& t) {
-    std::vector<Bucket> bs(buckets.begin(), buckets.begin() + multi_buckets(buckets));
+// [lo, hi): the KR <= 16 buckets (sw_multi_kernel) or the KR 17..24 ones (its
+// wide instance).
+void fill_multi(const std::vector<Bucket>& buckets, size_t lo, size_t hi, const Scheme& sch, msw::MultiTable& t) {
+    std::vector<Bucket> bs(buckets.begin() + lo, buckets.begin() + hi);
     auto cost = [](const Bucket& b) { return (uint64_t)msw::rows_per_lane(b.max_m, false) * (b.max_n + 16u); };
     std::stable_sort(bs.begin(), bs.end(), [&](const Bucket& a, const Bucket& b) { return cost(a) > cost(b); });
     memset(&t, 0, sizeof(t));
@@ -659,6 +661,10 @@ int join_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
     return MSW_OK;
 }
 
+// The KR 17..24 buckets as one launch (MSW_NO_WIDE_MULTI: one launch each,
+// for A/B runs).
+bool use_wide_multi(size_t n_wide) { return use_multi(n_wide) && !getenv("MSW_NO_WIDE_MULTI"); }
+
 int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const std::vector<Bucket>& buckets,
                    bool use_order, uint32_t read_stride, uint32_t win_stride) {
     const size_t n_short = short_buckets(buckets);
@@ -706,11 +712,36 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.out_by_slot = 1;
         p.out_slot_base = 0;
         msw::MultiTable t;
-        fill_multi(buckets, sch, t);
+        fill_multi(buckets, 0, n_multi, sch, t);
         HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
-        first_single = n_multi;  // the KR 17..24 buckets follow on their own
+        first_single = n_multi;
     }
-    for (size_t bi = first_single; bi < n_short; ++bi) {
+    // the KR 17..24 buckets: one launch of the wide instance when there are
+    // several (one launch each left each bucket's few waves running alone)
+    size_t single_end = n_short;
+    if (use_order && use_wide_multi(n_short - n_multi)) {
+        msw::SwParams p = base_params(sch);
+        p.reads = s.d_reads;
+        p.wins = s.d_wins;
+        p.read_len = s.d_rlen;
+        p.win_len = s.d_wlen;
+        p.order = s.d_order;
+        p.score = s.d_score;
+        p.end_i = sch.coords ? s.d_ei : nullptr;
+        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.read_stride = read_stride;
+        p.win_stride = win_stride;
+        p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+        p.group_lanes = 16;
+        p.groups = 4;
+        p.out_by_slot = 1;
+        p.out_slot_base = 0;
+        msw::MultiTable t;
+        fill_multi(buckets, n_multi, n_short, sch, t);
+        HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
+        single_end = n_multi;
+    }
+    for (size_t bi = first_single; bi < single_end; ++bi) {
         const Bucket& b = buckets[bi];
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
@@ -1285,6 +1316,8 @@ struct msw_plan {
     uint32_t* d_slot_lens = nullptr;  // read_len | win_len << 16 in slot order
     bool multi = false;
     msw::MultiTable table{};
+    bool wide = false;  // the KR 17..24 buckets as one launch (wide_table)
+    msw::MultiTable wide_table{};
     // packed-kernel buckets launched on their own (all of them without a
     // multi table, else the KR 17..24 ones), each with its layout
     std::vector<std::pair<Bucket, LaunchPlan>> singles;
@@ -1328,8 +1361,10 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
         }
         const size_t n_multi = multi_buckets(buckets);
         pl->multi = use_multi(n_multi);
-        if (pl->multi) fill_multi(buckets, sch, pl->table);
-        for (size_t bi = pl->multi ? n_multi : 0; bi < n_short; ++bi)
+        if (pl->multi) fill_multi(buckets, 0, n_multi, sch, pl->table);
+        pl->wide = use_wide_multi(n_short - n_multi);
+        if (pl->wide) fill_multi(buckets, n_multi, n_short, sch, pl->wide_table);
+        for (size_t bi = pl->multi ? n_multi : 0; bi < (pl->wide ? n_multi : n_short); ++bi)
             pl->singles.push_back({buckets[bi], choose_layout(buckets[bi].count, buckets[bi].max_m, buckets[bi].max_n,
                                                               sch, ctx->cu_count)});
         rc = grow_dev(&pl->d_order, n_pairs);
@@ -1405,7 +1440,7 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
         q.order = plan->d_order + plan->longs.begin;
         q.out_slot_base = plan->longs.begin;
         q.slot_lens = nullptr;
-        const bool beside = plan->multi || !plan->singles.empty();
+        const bool beside = plan->multi || plan->wide || !plan->singles.empty();
         if (beside && (rc = fork_side(ctx, st, side))) return rc;
         if ((rc = launch_long(sch, q, plan->longs.count, plan->longs.max_m, plan->longs.max_n, plan->longs.spread,
                               ctx->cu_count, beside ? ctx->side : st)))
@@ -1416,6 +1451,12 @@ int msw_align_batch_planned(msw_ctx* ctx, const msw_plan* plan, const msw_batch_
         q.group_lanes = 16;
         q.groups = 4;
         HIP_TRY(msw::launch_sw_multi(q, plan->table, sch.affine, sch.coords, st));
+    }
+    if (plan->wide) {
+        msw::SwParams q = p;
+        q.group_lanes = 16;
+        q.groups = 4;
+        HIP_TRY(msw::launch_sw_multi(q, plan->wide_table, sch.affine, sch.coords, st));
     }
     for (const auto& sb : plan->singles) {  // slots [b.begin, b.begin + count)
         const Bucket& b = sb.first;

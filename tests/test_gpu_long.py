@@ -106,6 +106,33 @@ def test_long_random_batch(gpu_ctx, oracle, kind):
                 oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc), sc.want_coords)
 
 
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_wide_buckets_one_launch(gpu_ctx, oracle, kind):
+    """Reads of 200..384 bases: the KR <= 16 buckets in one length-bucketed
+    launch and the KR 17..24 buckets (257..384) in one launch of its wide
+    instance -- host batches (one chunk and several) and a plan."""
+    import torch
+    sc = scoring(kind)
+    b = make_pairs(600, (200, 384), seed=31)
+    want = oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc)
+    for chunk in (0, 97):
+        assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc, chunk_pairs=chunk), want,
+                    sc.want_coords)
+    n = b.n_pairs
+    dR, dW, drl, dwl = _device([b.reads, b.wins, b.read_len.view(np.int16), b.win_len.view(np.int16)])
+    score, ei, ej = _device([np.zeros(n, np.int32), np.zeros(n, np.int16), np.zeros(n, np.int16)])
+    launch = gpu_ctx.prepare_planned_launch(dR.data_ptr(), drl.data_ptr(), dW.data_ptr(), dwl.data_ptr(),
+                                            b.reads.shape[1], b.wins.shape[1], b.read_len, b.win_len,
+                                            score.data_ptr(), sc, ei.data_ptr(), ej.data_ptr())
+    try:
+        launch()
+        gpu_ctx.synchronize()
+        torch.cuda.synchronize()
+        assert_same((score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy()), want, sc.want_coords)
+    finally:
+        launch.close()
+
+
 @pytest.mark.parametrize("blocks", ["1", "7", "0"])
 @pytest.mark.parametrize("kind", ["linear", "affine_coords"])
 def test_long_work_queue(gpu_ctx, oracle, monkeypatch, kind, blocks):

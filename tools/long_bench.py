@@ -29,7 +29,7 @@ def main():
     cases = [("300x600", 40_000, 300, 2.0, False), ("1000x2000", 4_000, 1000, 2.0, False),
              ("150x5000", 8_000, 150, 5000 / 150, False), ("150x300_forced", 10_000, 150, 2.0, True),
              ("150x300_packed", 10_000, 150, 2.0, False), ("mixed_257-2000x2", 8_000, (257, 2000), 2.0, False),
-             ("mixed_500-2000x2", 8_000, (500, 2000), 2.0, False)]
+             ("mixed_500-2000x2", 8_000, (500, 2000), 2.0, False), ("mixed_75-384x2", 100_000, (75, 384), 2.0, False)]
     for name, n, m, wf, force in cases:
         if args.only not in name:
             continue
