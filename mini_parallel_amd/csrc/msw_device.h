@@ -1205,25 +1205,25 @@ __global__ __launch_bounds__(64) void sw_multi_kernel(SwParams p, MultiTable t) 
             case 23: multi_body<23, AFFINE, COORDS>(q, blk, lds); break;
             default: multi_body<24, AFFINE, COORDS>(q, blk, lds); break;
         }
-        return;
-    }
-    switch (t.kr[b]) {
-        case 1: multi_body<1, AFFINE, COORDS>(q, blk, lds); break;
-        case 2: multi_body<2, AFFINE, COORDS>(q, blk, lds); break;
-        case 3: multi_body<3, AFFINE, COORDS>(q, blk, lds); break;
-        case 4: multi_body<4, AFFINE, COORDS>(q, blk, lds); break;
-        case 5: multi_body<5, AFFINE, COORDS>(q, blk, lds); break;
-        case 6: multi_body<6, AFFINE, COORDS>(q, blk, lds); break;
-        case 7: multi_body<7, AFFINE, COORDS>(q, blk, lds); break;
-        case 8: multi_body<8, AFFINE, COORDS>(q, blk, lds); break;
-        case 9: multi_body<9, AFFINE, COORDS>(q, blk, lds); break;
-        case 10: multi_body<10, AFFINE, COORDS>(q, blk, lds); break;
-        case 11: multi_body<11, AFFINE, COORDS>(q, blk, lds); break;
-        case 12: multi_body<12, AFFINE, COORDS>(q, blk, lds); break;
-        case 13: multi_body<13, AFFINE, COORDS>(q, blk, lds); break;
-        case 14: multi_body<14, AFFINE, COORDS>(q, blk, lds); break;
-        case 15: multi_body<15, AFFINE, COORDS>(q, blk, lds); break;
-        default: multi_body<16, AFFINE, COORDS>(q, blk, lds); break;
+    } else {
+        switch (t.kr[b]) {
+            case 1: multi_body<1, AFFINE, COORDS>(q, blk, lds); break;
+            case 2: multi_body<2, AFFINE, COORDS>(q, blk, lds); break;
+            case 3: multi_body<3, AFFINE, COORDS>(q, blk, lds); break;
+            case 4: multi_body<4, AFFINE, COORDS>(q, blk, lds); break;
+            case 5: multi_body<5, AFFINE, COORDS>(q, blk, lds); break;
+            case 6: multi_body<6, AFFINE, COORDS>(q, blk, lds); break;
+            case 7: multi_body<7, AFFINE, COORDS>(q, blk, lds); break;
+            case 8: multi_body<8, AFFINE, COORDS>(q, blk, lds); break;
+            case 9: multi_body<9, AFFINE, COORDS>(q, blk, lds); break;
+            case 10: multi_body<10, AFFINE, COORDS>(q, blk, lds); break;
+            case 11: multi_body<11, AFFINE, COORDS>(q, blk, lds); break;
+            case 12: multi_body<12, AFFINE, COORDS>(q, blk, lds); break;
+            case 13: multi_body<13, AFFINE, COORDS>(q, blk, lds); break;
+            case 14: multi_body<14, AFFINE, COORDS>(q, blk, lds); break;
+            case 15: multi_body<15, AFFINE, COORDS>(q, blk, lds); break;
+            default: multi_body<16, AFFINE, COORDS>(q, blk, lds); break;
+        }
     }
 }
 

@@ -108,17 +108,20 @@ size_t member_size(const uint8_t* h) {
 
 uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 
-// Whole members of buf[0, n) whose output fits in out_cap more bytes: appended
-// to mem (coff relative to buf, ooff from out_base).  *used = bytes of those
-// members.  Returns MSW_OK, or MSW_E_INVALID for data that is not BGZF.
-int index_members(const uint8_t* buf, size_t n, uint64_t out_base, uint64_t out_cap, std::vector<msw::GzMember>& mem,
-                  size_t* used, uint64_t* out_bytes) {
+// Whole members of buf[0, n) whose output fits in out_cap more bytes and
+// whose compressed bytes fit in in_cap: appended to mem (coff relative to buf,
+// ooff from out_base).  *used = bytes of those members (<= in_cap: members of
+// ISIZE 0, e.g. runs of BGZF EOF blocks, add compressed bytes but no output,
+// so the output cap alone does not bound the staging copy).  Returns MSW_OK,
+// or MSW_E_INVALID for data that is not BGZF.
+int index_members(const uint8_t* buf, size_t n, uint64_t out_base, uint64_t out_cap, size_t in_cap,
+                  std::vector<msw::GzMember>& mem, size_t* used, uint64_t* out_bytes) {
     size_t p = 0;
     uint64_t ob = 0;
     while (p + 18 <= n) {
         const size_t sz = member_size(buf + p);
         if (sz < 26) return set_error(MSW_E_INVALID, "not a BGZF block (mixed gzip members are not supported)");
-        if (p + sz > n) break;
+        if (p + sz > n || p + sz > in_cap) break;
         const uint32_t isize = le32(buf + p + sz - 4), crc = le32(buf + p + sz - 8);
         if (isize > 65536) return set_error(MSW_E_INVALID, "BGZF block larger than 64 KiB");
         if (ob + isize > out_cap) break;
@@ -423,10 +426,15 @@ void start_filler(msw_gfastq* g) {
     if (g->fread_off >= g->fsize || g->hc_len >= g->hc_cap) return;
     const size_t want = g->cur < 0 ? g->hc_cap : std::min(g->hc_cap, g->hc_len + g->last_used + kReadPiece);
     g->fill_rc = 0;
-    g->filler = std::thread([g, want]() {
-        g->fill_rc = fill_compressed(g, want);
-        if (g->fill_rc) g->fill_msg = msw_last_error();  // thread-local: carried to the caller's thread
-    });
+    try {
+        g->filler = std::thread([g, want]() {
+            g->fill_rc = fill_compressed(g, want);
+            if (g->fill_rc) g->fill_msg = msw_last_error();  // thread-local: carried to the caller's thread
+        });
+    } catch (const std::exception&) {
+        // no thread to spare: no read-ahead; next_span tops hc up inline
+        // (its own fill_compressed loop), so nothing escapes the C ABI
+    }
 }
 
 double now_ms() {
@@ -445,7 +453,7 @@ int next_span(msw_gfastq* g) {
     size_t used = 0;
     uint64_t obytes = 0;
     for (;;) {
-        if ((rc = index_members(g->hc, g->hc_len, kCarry, g->span, g->mem, &used, &obytes))) return rc;
+        if ((rc = index_members(g->hc, g->hc_len, kCarry, g->span, g->hc_cap, g->mem, &used, &obytes))) return rc;
         const bool full = obytes + 65536 > g->span || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
         if (full) break;
         g->mem.clear();
@@ -744,13 +752,14 @@ int msw_bgzf_inflate(msw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t* o
     uint8_t* hstage = nullptr;
     const char* ge = getenv("MSW_GZ_GROUP_MB");  // output bytes per launch (tools/inflate_bench.py)
     const uint64_t kGroup = (ge && atoll(ge) > 0 ? (uint64_t)atoll(ge) : 1024u) << 20;  // ~16k members: two waves per SIMD slot
+    const size_t kStage = (size_t)(kGroup + kGroup / 8 + (4u << 20));  // pinned staging: a group's compressed bytes
     uint64_t p = 0, total = 0;
     std::vector<msw::GzMember> mem;
     while (!rc && p < len) {
         mem.clear();
         size_t used = 0;
         uint64_t ob = 0;
-        rc = index_members(data + p, (size_t)(len - p), 0, kGroup, mem, &used, &ob);
+        rc = index_members(data + p, (size_t)(len - p), 0, kGroup, kStage, mem, &used, &ob);
         if (rc) break;
         if (mem.empty()) {
             rc = set_error(MSW_E_INVALID, "unexpected end of file");
@@ -764,7 +773,7 @@ int msw_bgzf_inflate(msw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t* o
             rc = set_error(MSW_E_NOMEM, "hipMalloc failed");
             break;
         }
-        if (!hstage && hipHostMalloc((void**)&hstage, kGroup + kGroup / 8 + (4u << 20)) != hipSuccess) {
+        if (!hstage && hipHostMalloc((void**)&hstage, kStage) != hipSuccess) {
             rc = set_error(MSW_E_NOMEM, "hipHostMalloc failed");
             break;
         }

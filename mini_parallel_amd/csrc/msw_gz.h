@@ -102,7 +102,7 @@ struct ParseBufs {
     uint32_t* vidx;         // (non-ASCII spans) per line: valid flag, then valid index or ~0u
     uint32_t* vline;        // (non-ASCII spans) valid index -> line index
     uint32_t* blk;          // scan scratch, line_cap / 1024 + 2 entries
-    uint32_t stride;        // slab row bytes (multiple of 16, <= 256 checked by the host)
+    uint32_t stride;        // slab row bytes (multiple of 16, <= 32768 checked by the host)
     ParseState* state;
     ParseOut* out;
 };
