@@ -1132,7 +1132,8 @@ std::string stable_run_id(const std::string& dir, const std::string& sample, con
     std::string key = dir + "|" + sample + "|" + a.score_mode + "|" + a.gap_model + "|" + a.reference + "|" +
                       env_or("GPU_CHUNK_SIZE_READS", "") + "|" + std::to_string(a.match) + "|" +
                       std::to_string(a.mismatch) + "|" + std::to_string(a.gap_open) + "|" +
-                      std::to_string(a.gap_extend) + "|" + std::to_string(a.window);
+                      std::to_string(a.gap_extend) + "|" + std::to_string(a.window) + "|" +
+                      env_or("WGS_FILE_SHARD", "");
     uint64_t h = 1469598103934665603ull;
     for (unsigned char c : key) { h ^= c; h *= 1099511628211ull; }
     char buf[32];
@@ -1171,6 +1172,20 @@ int main(int argc, char** argv) {
                 snprintf(name, sizeof(name), "%s/%s_L%03d_R%d_001.fastq.gz", dir.c_str(), sample.c_str(), lane, r);
                 files.push_back(name);
             }
+        // WGS_FILE_SHARD=r/N: this process takes lane files r, r+N, r+2N, ...
+        // (one process per GPU, e.g. bench.py's config-4 leg under
+        // torch.distributed.run; the reference has no multi-GPU path, gpu.rs:117,125)
+        const std::string shard = env_or("WGS_FILE_SHARD", "");
+        if (!shard.empty()) {
+            int r = -1, n = 0;
+            char tail = 0;
+            if (sscanf(shard.c_str(), "%d/%d%c", &r, &n, &tail) != 2 || n < 1 || r < 0 || r >= n)
+                die("error: WGS_FILE_SHARD must be r/N with 0 <= r < N, got '" + shard + "'");
+            std::vector<std::string> mine;
+            for (size_t i = (size_t)r; i < files.size(); i += (size_t)n) mine.push_back(files[i]);
+            files.swap(mine);
+            printf("File shard %d/%d: %zu lane file(s)\n", r, n, files.size());
+        }
         Checkpoint ck;
         ck.run_id = stable_run_id(dir, sample, a);
         ck.path = a.checkpoint_dir + "/checkpoint_" + ck.run_id + ".json";
@@ -1246,7 +1261,8 @@ int main(int argc, char** argv) {
           << ", \"total_score\": " << total << ", \"total_time_seconds\": " << secs << ", \"wall_ms\": " << rep.wall_ms
           << ", \"throughput_reads_per_second\": " << reads / secs
           << ", \"throughput_bases_per_second\": " << bases / secs << ", \"chunk_size\": " << get_chunk_size_reads()
-          << ", \"cpu_cores_used\": " << rep.readers << ", \"parallel_files\": " << (rep.readers > 1 ? "true" : "false")
+          << ", \"cpu_cores_used\": " << usable_cpus() << ", \"host_reader_threads\": " << rep.readers
+          << ", \"parallel_files\": " << (rep.readers > 1 || rep.host_threads > 1 ? "true" : "false")
           << ", \"system_info\": {\"gpu_name\": \"" << json_escape(devices.empty() ? "" : devices[0].name)
           << "\", \"gpu_memory_gb\": " << (devices.empty() ? 0.0 : devices[0].memory_gb)
           << ", \"cpu_cores\": " << std::thread::hardware_concurrency() << ", \"total_ram_gb\": " << ram_gb << "}"

@@ -39,6 +39,19 @@ def genome(n_bases: int, rng: np.random.Generator) -> np.ndarray:
     return ACGT[rng.integers(0, 4, n_bases, dtype=np.uint8)]
 
 
+def _rows(g: np.ndarray, start: np.ndarray, width: int) -> np.ndarray:
+    """rows[i] = g[start[i] : start[i] + width], indices past the end clamped
+    to the last base (g[min(start + c, len - 1)]), as a u8 copy: a gather
+    through a sliding-window view of g padded with its last base, instead of
+    an int64 index array of n x width entries."""
+    n = int(start.shape[0])
+    if n == 0 or width == 0:
+        return np.zeros((n, width), np.uint8)
+    pad = np.full(width, g[-1], np.uint8)
+    view = np.lib.stride_tricks.sliding_window_view(np.concatenate([g, pad]), width)
+    return view[np.asarray(start, np.int64)]
+
+
 def make_pairs(n_pairs: int, read_len, win_factor: float = 2.0, seed: int = 1002,
                genome_bases: int = 1 << 22, unrelated: float = 0.10, read_stride: int = 0,
                win_stride: int = 0, sub: float = 0.01, indel: float = 0.001,
@@ -64,12 +77,12 @@ def make_pairs(n_pairs: int, read_len, win_factor: float = 2.0, seed: int = 1002
     assert rs >= max_m and ws >= max_n, "stride smaller than the longest sequence"
     pos = rng.integers(0, genome_bases - max(max_n, 1), n_pairs)
     cols_w = np.arange(ws)
-    wins = g[np.minimum(pos[:, None] + cols_w[None, :], genome_bases - 1)]
+    wins = _rows(g, pos, ws)
     wins[cols_w[None, :] >= wlens[:, None]] = 0
     # read = genome[off : off + m], centred in the window
     off = pos + (wlens - lens) // 2
     cols_r = np.arange(rs)
-    reads = g[np.minimum(off[:, None] + cols_r[None, :], genome_bases - 1)]
+    reads = _rows(g, off, rs)
     valid = cols_r[None, :] < lens[:, None]
     subs = (rng.random(reads.shape) < sub) & valid
     idx = np.searchsorted(ACGT, reads[subs])
@@ -189,18 +202,48 @@ def bgzf_compress(data: bytes, level: int = 1, strategy: int = 0, block: int = 0
     return b"".join(out)
 
 
+def _lane_reads(g, k, reads_per_file, read_len, win_factor, seed):
+    """The reads of lane file k of a write_wgs_dataset run and their window
+    positions (every read gets a window of the genome: unrelated reads, pos
+    -1 in make_pairs, are paired with a random window), plus the rng the
+    writer continues with for the quality strings."""
+    genome_bases = int(g.shape[0])
+    b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_arr=g,
+                   read_stride=(read_len + 16 + 15) // 16 * 16)
+    rng = np.random.default_rng([seed, k])
+    span = genome_bases - int(b.win_len.max())
+    pos = np.where(b.pos >= 0, np.minimum(b.pos, span), rng.integers(0, span, b.n_pairs))
+    return b, pos, rng
+
+
+def _with_windows(g, b, pos) -> PairBatch:
+    cols = np.arange(b.wins.shape[1])
+    wins = _rows(g, pos, b.wins.shape[1])
+    wins[cols[None, :] >= b.win_len[:, None].astype(np.int64)] = 0
+    return PairBatch(b.reads, b.read_len.copy(), wins, b.win_len.copy(), pos)
+
+
+def wgs_genome(seed: int = 1004, genome_bases: int = 1 << 20) -> np.ndarray:
+    """The genome write_wgs_dataset writes as reference.fa for this seed."""
+    return genome(genome_bases, np.random.default_rng(seed))
+
+
+def lane_file_batch(k: int, reads_per_file: int, read_len: int = 150, win_factor: float = 2.0,
+                    seed: int = 1004, genome_bases: int = 1 << 20, genome_arr: np.ndarray | None = None) -> PairBatch:
+    """Lane file k (0-based, lane-major: L001_R1, L001_R2, L002_R1, ...) of a
+    write_wgs_dataset run with these parameters, regenerated without writing
+    it: its reads (file order) paired with their genome windows -- what the
+    oracle scores to check the --full-wgs per-file sums."""
+    g = wgs_genome(seed, genome_bases) if genome_arr is None else genome_arr
+    b, pos, _ = _lane_reads(g, k, reads_per_file, read_len, win_factor, seed)
+    return _with_windows(g, b, pos)
+
+
 def _write_lane_file(job):
     """One lane file of write_wgs_dataset (a process-pool job)."""
     import gzip
     (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep, bgzf, qual) = job
-    genome_bases = int(g.shape[0])
-    b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_arr=g,
-                   read_stride=(read_len + 16 + 15) // 16 * 16)
-    # every read gets a window of this genome: unrelated reads (pos -1) are
-    # paired with a random window
-    rng = np.random.default_rng([seed, k])
-    span = genome_bases - int(b.win_len.max())
-    pos = np.where(b.pos >= 0, np.minimum(b.pos, span), rng.integers(0, span, b.n_pairs))
+    b, pos, rng = _lane_reads(g, k, reads_per_file, read_len, win_factor, seed)
     rl = b.read_len.astype(np.int64)
     tag = sample.encode()
     if qual == "I":
@@ -229,10 +272,7 @@ def _write_lane_file(job):
             f.write(b"".join(recs))
     if not keep:
         return None
-    cols = np.arange(b.wins.shape[1])
-    wins = g[np.minimum(pos[:, None] + cols[None, :], genome_bases - 1)]
-    wins[cols[None, :] >= b.win_len[:, None].astype(np.int64)] = 0
-    return PairBatch(b.reads, b.read_len.copy(), wins, b.win_len.copy(), pos)
+    return _with_windows(g, b, pos)
 
 
 def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_per_lane: int = 2,
@@ -249,8 +289,7 @@ def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_p
     4-level) or "illumina" (Q2-Q41 drifting down the read, noisy)."""
     import os
     os.makedirs(out_dir, exist_ok=True)
-    rng = np.random.default_rng(seed)
-    g = genome(genome_bases, rng)
+    g = wgs_genome(seed, genome_bases)
     with open(os.path.join(out_dir, "reference.fa"), "w") as f:
         f.write(">synthetic seed=%d\n" % seed)
         s = g.tobytes().decode()

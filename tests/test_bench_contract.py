@@ -17,9 +17,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-def test_bench_json_line():
+def test_bench_json_line(tmp_path):
     cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--pairs", "2000",
-           "--cpu-seconds", "1", "--no-pcie"]
+           "--cpu-seconds", "1", "--no-pcie", "--c3-pairs", "20000", "--c5-pairs", "10000",
+           "--c4-reads-per-file", "20000", "--c4-dir", str(tmp_path / "c4")]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.strip().splitlines() if l.startswith("{")]
@@ -43,6 +44,22 @@ def test_bench_json_line():
     assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] in ("port", "reference")
     assert cpu["sample"]
     assert d["parity"]["bit_exact"] is True and d["parity"]["mismatches"] == 0
+    # VALU ceilings beside the instruction-mix one: SURVEY 8d's i32 ceiling
+    # and the lone-wave bound, for the headline and configs 3 / 5
+    for v in (d["valu"], d["configs_extra"]["config3"]["valu"], d["configs_extra"]["config5"]["valu"]):
+        for k in ("frac", "frac_i32_ceiling", "frac_lone_wave"):
+            assert 0 < v[k] < 1.5, (k, v[k])
+        assert abs(v["frac_i32_ceiling"] - v["kernel_gcups"] / v["i32_ceiling_gcups"]) < 1e-3
+    assert d["valu"]["i32_ceiling_gcups"] == pytest.approx(13107.2, abs=0.1)
+    assert d["configs_extra"]["config3"]["valu"]["i32_ceiling_gcups"] == pytest.approx(6049.5, abs=0.1)
+    ex = d["configs_extra"]
+    for c in ("config3", "config5"):
+        assert ex[c]["parity"]["bit_exact"] is True, c
+    h = ex["config3"]["host_to_host"]
+    assert h["equal_to_hbm_resident_run"] is True and h["value"] > 0 and h["chunk_pairs"] > 0
+    c4 = ex["config4"]
+    assert c4["parity"]["bit_exact"] is True and c4["reads"] == 16 * 20000
+    assert c4["reads_per_s"] >= c4["reads_per_s_incl_setup"] > 0 and c4["setup_ms"] > 0
 
 
 @pytest.mark.gpu

@@ -79,6 +79,56 @@ def test_single_rank_standin():
     _check(_json_line(r.stdout), 1)
 
 
+EXTRA = ["--cpu-standin", "--steps", "1", "--warmup", "0", "--pairs", "1000", "--cpu-seconds", "0", "--no-pcie",
+         "--extra-configs", "3,4,5", "--c3-pairs", "1500", "--c5-pairs", "1300", "--c4-reads-per-file", "120"]
+
+
+def _check_extras(d, world):
+    """configs_extra at N = world: configs 3 / 5 sharded over the ranks and
+    gathered in order, config 4's lane files sharded by file (each exactly
+    once) with the per-file rows gathered and file 0 recomputed."""
+    ex = d["configs_extra"]
+    for c, per in (("config3", 1500), ("config5", 1300)):
+        e = ex[c]
+        assert e["n_ranks"] == world and e["global_pairs"] == per * world and e["gathered_pairs"] == per * world
+        assert e["parity"]["gather_in_order"] is True, c
+        assert e["valu"]["frac_i32_ceiling"] >= 0 and e["valu"]["frac_lone_wave"] >= 0
+    c4 = ex["config4"]
+    assert c4["n_ranks"] == world and c4["files_per_rank"] == 16 // world and c4["scaling"] == "strong"
+    p = c4["parity"]
+    assert p["files_once"] and p["files_done"] == 16 and p["reads"] == p["reads_expected"] == 16 * 120
+    assert p["file0_ok"] is True
+    assert c4["reads_per_s"] > 0 and c4["gcups"] > 0
+
+
+@pytest.mark.parametrize("launch", ["self", "torchrun"])
+def test_two_ranks_run_every_config(tmp_path, launch):
+    args = EXTRA + ["--c4-dir", str(tmp_path / "c4")]
+    if launch == "self":
+        cmd = [sys.executable, "bench.py", "--gpus", "2"] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2"] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    _check(d, 2, per_gpu=1000)
+    _check_extras(d, 2)
+
+
+def test_one_rank_runs_every_config(tmp_path):
+    r = subprocess.run([sys.executable, "bench.py"] + EXTRA + ["--c4-dir", str(tmp_path / "c4")], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    _check_extras(d, 1)
+    v = d["valu"]
+    for k in ("frac", "frac_i32_ceiling", "frac_lone_wave"):  # a CPU stand-in rate: tiny, present
+        assert v[k] >= 0, k
+    assert v["ceiling_gcups"] > v["lone_wave_ceiling_gcups"] > 0 and v["i32_ceiling_gcups"] > 0
+    assert v["i32_ceiling_gcups"] == pytest.approx(13107.2, abs=0.1)  # SURVEY 8d: 13.1 TCUPS linear
+
+
 def test_shards_of_one_global_batch():
     """Pair i of the global batch is the same whichever range generates it."""
     whole = config_shard(5, 0, 2500)

@@ -248,6 +248,38 @@ def test_full_wgs_config4_shape_two_workers(tmp_path, oracle, gpu_inflate):
 
 
 @pytest.mark.gpu
+def test_full_wgs_file_shards(tmp_path, oracle):
+    """WGS_FILE_SHARD=r/N (bench.py's config-4 leg: one process per GPU, rank
+    r takes lane files r, r + N, ...): the two shards of a 2-way split cover
+    every file exactly once and their per-file sums are the oracle's; the
+    run record says cpu_cores_used = the CPUs the process may use
+    (num_cpus::get(), tools/benchmark.rs:119); a malformed shard is refused."""
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=3, reads_per_lane=2, reads_per_file=700, bgzf=True)
+    want = {os.path.basename(f): int(oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=8)[0]
+                                      .astype(np.int64).sum()) for f, b in zip(ds["files"], ds["batches"])}
+    got = {}
+    for r in range(2):
+        env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "3",
+               "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "300", "WGS_FILE_SHARD": f"{r}/2"}
+        res = run(["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
+                   "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / f"rec{r}.json")], env=env, cwd=tmp_path)
+        assert res.returncode == 0, res.stdout + res.stderr
+        assert f"File shard {r}/2: 3 lane file(s)" in res.stdout
+        rec = json.load(open(tmp_path / f"rec{r}.json"))
+        assert rec["cpu_cores_used"] == rec["host_cpus_usable"] >= 1
+        ck = json.load(open(tmp_path / f"checkpoint_{rec['run_id']}.json"))
+        for f in ck["files"]:
+            name = os.path.basename(f["file_path"])
+            assert name not in got
+            got[name] = f["score"]
+    assert got == want
+    env["WGS_FILE_SHARD"] = "2/2"
+    res = run(["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"]], env=env, cwd=tmp_path)
+    assert res.returncode == 1 and "WGS_FILE_SHARD must be r/N" in res.stderr
+
+
+@pytest.mark.gpu
 def test_num_gpus_beyond_visible_fails(tmp_path):
     from mini_parallel_amd.synthetic import write_wgs_dataset
     import torch
