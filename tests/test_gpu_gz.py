@@ -118,6 +118,22 @@ def test_inflate_large_many_spans(gpu_ctx):
     assert bgzf_inflate(gpu_ctx, blob) == data
 
 
+def test_inflate_long_run_of_empty_members(gpu_ctx, monkeypatch):
+    """members of ISIZE 0 (BGZF EOF blocks) add compressed bytes
+    but no output, so a group bounded only by its output size could copy
+    more compressed bytes than the pinned staging holds.  With 1 MiB groups
+    (staging 5.125 MiB) 250k EOF blocks (7 MB) between data members must
+    inflate in several groups, exactly as zlib reads them."""
+    from mini_parallel_amd.synthetic import BGZF_EOF
+    monkeypatch.setenv("MSW_GZ_GROUP_MB", "1")
+    data = fastq_text(3000, 16)
+    head = bgzf_compress(data[: len(data) // 2], 6, eof_block=False)
+    tail = bgzf_compress(data[len(data) // 2:], 6)
+    blob = head + BGZF_EOF * 250_000 + tail
+    assert len(blob) > 7_000_000
+    assert bgzf_inflate(gpu_ctx, blob) == data
+
+
 def test_inflate_errors(gpu_ctx):
     data = fastq_text(400, 13)
     blob = bytearray(bgzf_compress(data, 6))

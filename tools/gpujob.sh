@@ -1,0 +1,51 @@
+#!/bin/bash
+# One parametrised GPU job (replaces the round-1/2 tools/run_*.sh wrappers):
+#   bash tools/gpujob.sh TAG STEP [STEP ...]
+# Steps run in order, each under its own time limit; the first failure ends
+# the job (set -e), so nothing runs on the GPU after a fault or a kill.
+#   tests[=PYTEST_PATHS]   pytest -m gpu (default: tests), log gpurun_out/TAG/gputest.log
+#   smoke                  __graft_entry__.smoke()
+#   bench[=ARGS]           python3 bench.py ARGS > gpurun_out/TAG/bench.json
+#   prof                   rocprofv3 --kernel-trace --stats of the config-2 bench (gpurun_out/TAG/prof_c2)
+#   e2e[=ENVSETS]          tools/wgs_e2e.py over the config-4-shape BGZF set (16 x 2 M reads, binned, level 6);
+#                          ENVSETS as wgs_e2e.py --extra-env (default MSW_GPU_INFLATE=1)
+#   longbench              tools/long_bench.py
+# Example: gpurun --timeout 1200 -- bash tools/gpujob.sh r03a tests smoke bench prof
+set -euo pipefail
+T=${1:?tag}
+shift
+OUT=gpurun_out/$T
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for step in "$@"; do
+  name=${step%%=*}
+  arg=""
+  [[ "$step" == *=* ]] && arg=${step#*=}
+  case "$name" in
+    tests)
+      # shellcheck disable=SC2086
+      bash tools/gpu_tests.sh "$T" ${arg:-tests} ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      echo "smoke: $(tail -1 "$OUT/smoke.log")" ;;
+    bench)
+      # shellcheck disable=SC2086
+      timeout -k 10 600 python3 bench.py $arg > "$OUT/bench.json" 2> "$OUT/bench.err"
+      echo "bench: $(head -c 300 "$OUT/bench.json")" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c2" -o t --output-format csv -- \
+        python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-pcie --extra-configs none \
+        > "$OUT/prof_c2.log" 2>&1
+      echo "prof ok" ;;
+    e2e)
+      timeout -k 10 900 python3 tools/wgs_e2e.py --dir /tmp/msw_gz_e2e --reads-per-file 2000000 --bgzf \
+        --qual binned --level 6 --workers 16 --host-threads 16 --extra-env "${arg:-MSW_GPU_INFLATE=1}" \
+        --out "$OUT/e2e.jsonl" > "$OUT/e2e.log" 2> "$OUT/e2e.err"
+      echo "e2e: $(grep -o '"throughput_reads_per_second": [0-9.]*' "$OUT/e2e.jsonl" | tr '\n' ' ')" ;;
+    longbench)
+      timeout -k 10 300 python3 tools/long_bench.py > "$OUT/long_bench.jsonl" 2> "$OUT/long_bench.err"
+      echo "longbench ok" ;;
+    *)
+      echo "unknown step $name" >&2; exit 2 ;;
+  esac
+done
