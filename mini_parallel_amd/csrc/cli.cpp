@@ -676,11 +676,15 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         for (int wi = 0; wi < nworkers; ++wi) {
             workers.emplace_back([&, wi]() {
                 const int gi = wi % ngpu;
+                static const bool strace = getenv("MSW_SETUP_TRACE") != nullptr;  // setup phases to stderr
+                const auto ts0 = Clock::now();
                 Ctx ctx(devices[gi].ordinal);
+                const double t_ctx = ms_since(ts0);
                 const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
                 msw_genome* gen = nullptr;
                 if (msw_genome_create(ctx.h, (const uint8_t*)genome.data(), genome.size(), &gen) != MSW_OK)
                     die(std::string("GPU genome upload error: ") + msw_last_error());
+                const double t_gen = ms_since(ts0);
                 // two result sets: batch k's copy-back lands while batch k+1 runs
                 struct Res {
                     int32_t* d_score = nullptr;
@@ -757,8 +761,13 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 };
                 int cur = 0;
                 msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
+                const double t_res = ms_since(ts0);
                 if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
                     die(std::string("GPU lane reader: ") + msw_last_error());
+                if (strace)
+                    fprintf(stderr, "[setup] worker %d: context %.1f ms, genome %.1f ms, result sets %.1f ms, "
+                                    "lane reader %.1f ms\n", wi, t_ctx, t_gen - t_ctx, t_res - t_gen,
+                            ms_since(ts0) - t_res);
                 // the reader's stats of the file it just finished
                 auto reader_done = [&](size_t fi) {
                     uint64_t bi = 0, bo = 0;
