@@ -32,6 +32,7 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include "../../include/msw.h"
@@ -280,9 +281,23 @@ struct msw_gfastq {
     bool want_pos = false;
     uint64_t span = kDefaultSpan;
 
-    // compressed bytes read but not yet inflated: hc[0, hc_len)
+    // compressed bytes read but not yet inflated: hc[0, hc_len).  Two ways
+    // to get them (msw_fastq.h):
+    //  mapped (default): hc points into the file's read-only mapping; the
+    //    window [reg_lo, fread_off) of the page cache is pinned in place
+    //    (hipHostRegister) and DMA'd to the GPU -- no host copy, no pinned
+    //    staging allocation;
+    //  copied (MSW_GZ_NO_MAP=1, or when mapping / registering fails): preads
+    //    into hc_buf, a hipHostMalloc'ed staging buffer allocated on first use.
     uint8_t* hc = nullptr;
     size_t hc_cap = 0, hc_len = 0;
+    size_t in_cap = 0;                 // compressed bytes per span, either way
+    uint8_t* hc_buf = nullptr;         // copied mode's pinned staging (in_cap bytes)
+    bool mapped = false;
+    uint8_t* map = nullptr;            // whole-file mapping (mapped mode)
+    uint64_t map_off = 0;              // first byte not yet inflated
+    uint64_t reg_lo = 0, reg_len = 0;  // the registered window
+    bool reg_failed = false;
     // read-ahead: while the GPU inflates / the caller scores, a host thread
     // reads the next span's compressed bytes into hc after hc_len
     std::thread filler;
@@ -332,11 +347,14 @@ void join_filler(msw_gfastq* g) {
     if (g->filler.joinable()) g->filler.join();
 }
 
+void unmap_file(msw_gfastq* g);
+
 void release(msw_gfastq* g) {
     join_filler(g);
-    if (g->f) fclose(g->f);
     (void)hipSetDevice(g->device);
     if (g->rs) (void)hipStreamSynchronize(g->rs);
+    unmap_file(g);
+    if (g->f) fclose(g->f);
     for (int i = 0; i < 2; ++i) {
         if (g->dout[i]) (void)hipFree(g->dout[i]);
         if (g->s_reads[i]) (void)hipFree(g->s_reads[i]);
@@ -356,7 +374,7 @@ void release(msw_gfastq* g) {
     if (g->d_out) (void)hipFree(g->d_out);
     if (g->h_out) (void)hipHostFree(g->h_out);
     if (g->h_state) (void)hipHostFree(g->h_state);
-    if (g->hc) (void)hipHostFree(g->hc);
+    if (g->hc_buf) (void)hipHostFree(g->hc_buf);
     g->inf.release();
     if (g->parsed) (void)hipEventDestroy(g->parsed);
     for (hipEvent_t e : g->emitted)
@@ -421,8 +439,36 @@ int fill_compressed(msw_gfastq* g, size_t want);
 // Start reading ahead ~one span's compressed bytes (the last span's size; a
 // whole staging buffer at the start of a file) in the background; next_span
 // joins before it touches hc.
+// Mapped mode: pin the next window of the mapping, [map_off rounded down to
+// a page, + in_cap), in the background (cached pages register at ~200 GB/s,
+// tools/host_feed.cpp; cold ones are read from disk here).
+void register_window(msw_gfastq* g) {
+    const uint64_t lo = g->map_off & ~(uint64_t)4095;
+    const uint64_t hi = std::min<uint64_t>(g->fsize, lo + g->in_cap);
+    if (hipSetDevice(g->device) != hipSuccess ||
+        hipHostRegister(g->map + lo, (size_t)(hi - lo), hipHostRegisterReadOnly) != hipSuccess) {
+        (void)hipGetLastError();
+        g->reg_failed = true;  // next_span falls back to copies
+        return;
+    }
+    g->reg_lo = lo;
+    g->reg_len = hi - lo;
+    g->hc = g->map + g->map_off;
+    g->hc_len = g->hc_cap = (size_t)(hi - g->map_off);
+    g->fread_off = hi;
+}
+
 void start_filler(msw_gfastq* g) {
     join_filler(g);
+    if (g->mapped) {
+        if (g->map_off >= g->fsize || g->reg_len) return;
+        try {
+            g->filler = std::thread([g]() { register_window(g); });
+        } catch (const std::exception&) {
+            register_window(g);
+        }
+        return;
+    }
     if (g->fread_off >= g->fsize || g->hc_len >= g->hc_cap) return;
     const size_t want = g->cur < 0 ? g->hc_cap : std::min(g->hc_cap, g->hc_len + g->last_used + kReadPiece);
     g->fill_rc = 0;
@@ -437,6 +483,37 @@ void start_filler(msw_gfastq* g) {
     }
 }
 
+// copied mode's pinned staging, allocated on first use
+int ensure_stage(msw_gfastq* g) {
+    if (!g->hc_buf && hipHostMalloc((void**)&g->hc_buf, g->in_cap, hipHostMallocDefault) != hipSuccess) {
+        g->hc_buf = nullptr;
+        return set_error(MSW_E_NOMEM, "hipHostMalloc failed (GPU lane reader staging)");
+    }
+    return MSW_OK;
+}
+
+// after the stream drained: unpin the window, drop the mapping
+void unmap_file(msw_gfastq* g) {
+    if (g->reg_len) (void)hipHostUnregister(g->map + g->reg_lo);
+    if (g->map) munmap(g->map, (size_t)g->fsize);
+    g->map = nullptr;
+    g->mapped = false;
+    g->reg_lo = g->reg_len = 0;
+}
+
+// A window could not be pinned: the rest of the file goes through copies.
+int to_copied(msw_gfastq* g) {
+    const uint64_t off = g->map_off;
+    unmap_file(g);
+    int rc;
+    if ((rc = ensure_stage(g))) return rc;
+    g->hc = g->hc_buf;
+    g->hc_cap = g->in_cap;
+    g->hc_len = 0;
+    g->fread_off = off;
+    return fill_compressed(g, g->hc_cap);
+}
+
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -448,12 +525,15 @@ int next_span(msw_gfastq* g) {
     const int nx = 1 - g->last_buf;
     join_filler(g);
     if (g->fill_rc) return set_error(g->fill_rc, "%s", g->fill_msg.c_str());
+    if (g->mapped && g->reg_failed && (rc = to_copied(g))) return rc;
+    if (g->mapped && !g->reg_len && g->map_off < g->fsize) register_window(g);  // no read-ahead ran
+    if (g->mapped && g->reg_failed && (rc = to_copied(g))) return rc;
     // 1. whole members whose output fits the span (compressed <= span bytes + 1 MiB)
     g->mem.clear();
     size_t used = 0;
     uint64_t obytes = 0;
     for (;;) {
-        if ((rc = index_members(g->hc, g->hc_len, kCarry, g->span, g->hc_cap, g->mem, &used, &obytes))) return rc;
+        if ((rc = index_members(g->hc, g->hc_len, kCarry, g->span, g->in_cap, g->mem, &used, &obytes))) return rc;
         const bool full = obytes + 65536 > g->span || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
         if (full) break;
         g->mem.clear();
@@ -474,8 +554,12 @@ int next_span(msw_gfastq* g) {
     // before the current one (long finished, normally); the current span's
     // emits and the caller's scoring keep running
     if (g->emitted_valid[nx]) GZ_TRY(hipStreamWaitEvent(s, g->emitted[nx], 0));
-    // 2. inflate + CRC into dout[nx] at kCarry
-    if ((rc = g->inf.run(g->hc, used, g->mem, g->dout[nx], s))) return rc;
+    // 2. inflate + CRC into dout[nx] at kCarry (mapped: the upload starts at
+    // the page boundary below hc, inside the registered window)
+    const size_t lead = g->mapped ? (size_t)(g->map_off - g->reg_lo) : 0;
+    if (lead)
+        for (msw::GzMember& m : g->mem) m.coff += lead;
+    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s))) return rc;
     // 3. the previous span's unfinished line goes right in front
     const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
     if (carry > kCarry)
@@ -507,7 +591,13 @@ int next_span(msw_gfastq* g) {
     const double t_a = trace ? now_ms() : 0.0;
     if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
     // the upload of hc has completed: drop the consumed bytes and read ahead
-    if (used) {
+    if (g->mapped) {
+        // the window's upload is done: unpin it; the next one registers in the background
+        (void)hipHostUnregister(g->map + g->reg_lo);
+        g->reg_len = 0;
+        g->map_off += used;
+        g->hc_len = 0;
+    } else if (used) {
         memmove(g->hc, g->hc + used, g->hc_len - used);
         g->hc_len -= used;
     }
@@ -566,11 +656,21 @@ int next_span(msw_gfastq* g) {
 // buffers kept.  The parse state goes back to line 0 on the reader stream.
 int open_file(msw_gfastq* g, const char* path) {
     join_filler(g);
+    if (g->mapped || g->map) {
+        // the previous file's last window may still be uploading
+        GZ_TRY(hipSetDevice(g->device));
+        GZ_TRY(hipStreamSynchronize(g->rs));
+        unmap_file(g);
+    }
     if (g->f) fclose(g->f);
     g->f = nullptr;
     g->path = path;
     g->fsize = g->fread_off = 0;
     g->hc_len = 0;
+    g->hc = g->hc_buf;
+    g->hc_cap = g->hc_buf ? g->in_cap : 0;
+    g->map_off = g->reg_lo = g->reg_len = 0;
+    g->reg_failed = false;
     g->cur = -1;
     g->cur_off = g->cur_len = g->tail_start = 0;
     g->started = g->at_eof = false;
@@ -598,6 +698,22 @@ int open_file(msw_gfastq* g, const char* path) {
         // the state); the previous file's batches stay valid on the caller's stream
         GZ_TRY(hipSetDevice(g->device));
         GZ_TRY(hipMemcpyAsync(g->d_state, g->d_state0, sizeof(msw::ParseState), hipMemcpyDeviceToDevice, g->rs));
+    }
+    const char* nm = getenv("MSW_GZ_NO_MAP");  // per file: tests switch it between readers
+    const bool no_map = nm && atoi(nm) != 0;
+    if (!no_map && g->fsize > 0) {
+        void* m = mmap(nullptr, (size_t)g->fsize, PROT_READ, MAP_SHARED, fileno(g->f), 0);
+        if (m != MAP_FAILED) {
+            g->map = (uint8_t*)m;
+            g->mapped = true;
+            (void)madvise(m, (size_t)g->fsize, MADV_SEQUENTIAL);
+        }
+    }
+    if (!g->mapped && g->fsize > 0) {
+        int rc;
+        if ((rc = ensure_stage(g))) return rc;
+        g->hc = g->hc_buf;
+        g->hc_cap = g->in_cap;
     }
     start_filler(g);  // the first span's compressed bytes, read while the caller finishes the last file
     return MSW_OK;
@@ -650,9 +766,8 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
         return bail(set_error(MSW_E_DEVICE, "stream/event creation failed"));
     // compressed staging: half a span (FASTQ compresses ~3-4x; less
     // compressible data just makes shorter spans) + room for one fread piece
-    g->hc_cap = (size_t)(std::max<uint64_t>(g->span / 2, 16u << 20) + kReadPiece + (1u << 20));
-    if (hipHostMalloc((void**)&g->hc, g->hc_cap, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&g->h_out, sizeof(msw::ParseOut), hipHostMallocDefault) != hipSuccess)
+    g->in_cap = (size_t)(std::max<uint64_t>(g->span / 2, 16u << 20) + kReadPiece + (1u << 20));
+    if (hipHostMalloc((void**)&g->h_out, sizeof(msw::ParseOut), hipHostMallocDefault) != hipSuccess)
         return bail(set_error(MSW_E_NOMEM, "hipHostMalloc failed (GPU lane reader staging)"));
     const size_t ob = (size_t)(kCarry + g->span + kPad);
     for (int i = 0; i < 2; ++i) {

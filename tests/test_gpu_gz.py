@@ -216,9 +216,15 @@ def assert_reader_parity(ctx, path, **kw):
     return len(hl)
 
 
+@pytest.mark.parametrize("mode", ["map", "copy"])
 @pytest.mark.parametrize("block", [0xFF00, 1000])
 @pytest.mark.parametrize("crlf", [False, True])
-def test_reader_matches_host_reader(gpu_ctx, tmp_path, block, crlf):
+def test_reader_matches_host_reader(gpu_ctx, tmp_path, monkeypatch, block, crlf, mode):
+    """mode "map": compressed bytes DMA'd straight from the file's mapping
+    (page-cache pages pinned in place, one window per span, uploads starting
+    at the page boundary below the span); "copy": preads into pinned staging
+    (MSW_GZ_NO_MAP=1)."""
+    monkeypatch.setenv("MSW_GZ_NO_MAP", "1" if mode == "copy" else "0")
     data = fastq_text(20_000, 21 + block % 7, crlf=crlf)  # ~7-8 MB: several 1 MiB spans, records straddle them
     p = tmp_path / "lane.fastq.gz"
     p.write_bytes(bgzf_compress(data, 6, block=block))
@@ -231,6 +237,7 @@ def test_reader_parallel_compressed_reads(gpu_ctx, tmp_path, monkeypatch, thread
     """Compressed top-ups split over several positioned-read threads
     (MSW_GZ_READ_THREADS; MSW_GZ_READ_SPLIT lowers the 32 MiB threshold so a
     small file takes the split path, with parts ending mid-member)."""
+    monkeypatch.setenv("MSW_GZ_NO_MAP", "1")
     monkeypatch.setenv("MSW_GZ_READ_THREADS", threads)
     monkeypatch.setenv("MSW_GZ_READ_SPLIT", "4099")
     data = fastq_text(20_000, 23)
@@ -239,7 +246,9 @@ def test_reader_parallel_compressed_reads(gpu_ctx, tmp_path, monkeypatch, thread
     assert assert_reader_parity(gpu_ctx, str(p)) == 20_000
 
 
-def test_reader_edge_files(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("mode", ["map", "copy"])
+def test_reader_edge_files(gpu_ctx, tmp_path, monkeypatch, mode):
+    monkeypatch.setenv("MSW_GZ_NO_MAP", "1" if mode == "copy" else "0")
     rng = np.random.default_rng(5)
     cases = {
         "empty": b"",
