@@ -131,6 +131,17 @@ struct PairMeta {
     int ma, mb, na, nb;
 };
 
+// Traffic probes (tools/traffic_split.sh, built by tools/build_variant.sh with
+// -DMSW_PROBE_NO_WIN=1 or -DMSW_PROBE_NO_READ=1): the window / read loads are
+// replaced by constants so rocprofv3 FETCH_SIZE of the variant splits a
+// launch's HBM reads by buffer.  Scores are wrong in a probe build.
+#ifndef MSW_PROBE_NO_WIN
+#define MSW_PROBE_NO_WIN 0
+#endif
+#ifndef MSW_PROBE_NO_READ
+#define MSW_PROBE_NO_READ 0
+#endif
+
 template <bool SPLIT>
 __device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t block, bool active) {
     // Branch-free: clamped indices keep every load legal (n_slots >= 1), the
@@ -224,7 +235,7 @@ __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& 
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int k = k0 + u * G + lg;
-                const bool ld = k < nch && k < loadable;
+                const bool ld = k < nch && k < loadable && !MSW_PROBE_NO_WIN;
                 va[u] = ld ? *reinterpret_cast<const uint4*>(wa + 16 * k) : make_uint4(0, 0, 0, 0);
                 if constexpr (SPLIT) {
                     prev[u] = wa[min(max(16 * k - 1, 0), last)];
@@ -293,8 +304,14 @@ __device__ __forceinline__ void load_read_bytes(const SwParams& p, uint32_t pa, 
     for (int r = 0; r < KR; ++r) {
         const int ia = SPLIT ? lg * 2 * KR + r : lg * KR + r;
         const int ib = SPLIT ? ia + KR : ia;
+#if MSW_PROBE_NO_READ
+        ba[r] = (uint32_t)(ia + pa) & 3u;
+        bb[r] = (uint32_t)(ib + pb) & 3u;
+        (void)ra; (void)rb; (void)last;
+#else
         ba[r] = ra[min(ia, last)];
         bb[r] = rb[min(ib, last)];
+#endif
     }
 }
 
@@ -510,9 +527,15 @@ __device__ __forceinline__ void load_round(const SwParams& p, uint32_t pa, uint3
     for (int u = 0; u < kRound; ++u) {
         // clamped chunk index: always a legal load; columns past the window are masked
         const int k = min(k0 + u * G + lg, top);
+#if MSW_PROBE_NO_WIN
+        w.a[u] = w.b[u] = make_uint4(0x03020100u + k, 0x01000302u, 0x02010003u, 0x00030201u ^ (uint32_t)pa);
+        w.prev[u] = 0;
+        (void)wa; (void)wb; (void)last;
+#else
         w.a[u] = *reinterpret_cast<const uint4*>(wa + 16 * k);
         if constexpr (SPLIT) w.prev[u] = wa[min(max(16 * (k0 + u * G + lg) - 1, 0), last)];
         else w.b[u] = *reinterpret_cast<const uint4*>(wb + 16 * k);
+#endif
     }
 }
 

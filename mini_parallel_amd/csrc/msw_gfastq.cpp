@@ -335,6 +335,8 @@ struct msw_gfastq {
 
     uint64_t span_reads = 0, span_done = 0, next_first = 0;
     uint32_t span_min = 0, span_max = 0;
+    uint64_t bucket_reads = 1;              // reads per span_bmax entry
+    uint32_t span_bmax[msw::kLenBuckets] = {};
     int failed = 0;  // sticky error code
 
     // stats
@@ -613,6 +615,11 @@ int next_span(msw_gfastq* g) {
         if ((rc = grow(&b.vline, &g->v_cap[nx], (size_t)nlines + 1))) return rc;
         if ((rc = grow(&b.blk, &g->blk_cap[nx], (size_t)(nlines / 1024 + 2)))) return rc;
     }
+    // read-length maxima per run of whole batches (<= kLenBuckets runs)
+    {
+        const uint64_t batches = (nlines / 4 + 1 + g->max_reads - 1) / g->max_reads;
+        b.bucket_reads = g->max_reads * ((batches + msw::kLenBuckets - 1) / msw::kLenBuckets);
+    }
     GZ_TRY(msw::launch_parse_b(b, nlines, any_high, s));
     GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
     GZ_TRY(hipEventRecord(g->parsed, s));
@@ -642,6 +649,8 @@ int next_span(msw_gfastq* g) {
     g->span_done = 0;
     g->span_min = o.min_len;
     g->span_max = o.max_len;
+    g->bucket_reads = b.bucket_reads;
+    memcpy(g->span_bmax, o.bmax, sizeof(g->span_bmax));
     g->sp.v0 = o.v0;
     g->sp.pending_in = o.pending_in;
     g->sp.any_high = o.any_high;
@@ -834,7 +843,8 @@ int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {
     out->n = n;
     out->first_read = g->next_first;
     out->min_len = g->span_min;
-    out->max_len = g->span_max;
+    // the batch's own longest read (its run of the span), not the span's
+    out->max_len = g->span_bmax[std::min<uint64_t>(g->span_done / g->bucket_reads, msw::kLenBuckets - 1)];
     g->span_done += n;
     g->next_first += n;
     return MSW_OK;

@@ -62,6 +62,7 @@ hipError_t launch_gz_crc(const uint8_t* out, const GzMember* members, uint32_t n
 // number (1-based, over the whole file) % 4 == 2 is a sequence.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kParseTile = 4096;  // bytes per line-count tile
+constexpr uint32_t kLenBuckets = 256;  // per-span read-length maxima (ParseOut::bmax)
 
 struct ParseState {   // device-resident, carried from span to span
     uint64_t valid_lines;   // valid lines of the file before this span
@@ -86,6 +87,10 @@ struct ParseOut {     // per span, read back by the host
     uint32_t err_over;      // the file passed 10 invalid lines in this span
     uint64_t too_long_line; // smallest valid line number (1-based, file) of such a line
     uint64_t err_line;      // valid lines read before the file's 11th invalid line
+    // longest read of each run of ParseBufs::bucket_reads reads of the span
+    // (a batch of the reader lies inside one run): the batch's bound, so one
+    // long read sends only its own batch to a wider kernel, not the span
+    uint32_t bmax[kLenBuckets];
 };
 
 struct ParseBufs {
@@ -103,6 +108,7 @@ struct ParseBufs {
     uint32_t* vline;        // (non-ASCII spans) valid index -> line index
     uint32_t* blk;          // scan scratch, line_cap / 1024 + 2 entries
     uint32_t stride;        // slab row bytes (multiple of 16, <= 32768 checked by the host)
+    uint64_t bucket_reads;  // reads per ParseOut::bmax entry (a multiple of the batch size; phase B)
     ParseState* state;
     ParseOut* out;
 };

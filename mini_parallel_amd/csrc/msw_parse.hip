@@ -258,6 +258,7 @@ __global__ __launch_bounds__(256) void k_scan_tiles(ParseBufs b) {
         pre += c;
     }
     const int anyh = __syncthreads_or(h != 0);
+    if (t < kLenBuckets) b.out->bmax[t] = 0;
     if (t == 0) {
         ParseOut* o = b.out;
         const bool final_line = b.eof && b.len > b.begin && b.buf[b.len - 1] != '\n';
@@ -390,6 +391,12 @@ __global__ __launch_bounds__(256) void k_vapply(ParseBufs b) {
 }
 
 // --- per read: lengths and the span totals ---------------------------------
+__device__ inline uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_lens(ParseBufs b) {
     ParseOut* o = b.out;
     if (o->overflow) return;
@@ -398,16 +405,45 @@ __global__ __launch_bounds__(256) void k_lens(ParseBufs b) {
     const uint32_t ph = seq_phase(v0);
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
     uint64_t bases = 0, tl = ~0ull;
-    for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256) {
-        const uint64_t j = ph + 4 * r;
-        const uint64_t k = ascii ? j : b.vline[j];
-        uint32_t st, en;
-        line_bounds(b, k, st, en);
-        const uint32_t len = en - st;
-        if (len > b.stride) tl = min(tl, v0 + j + 1);
-        mn = min(mn, len);
-        mx = max(mx, len);
-        bases += len;
+    // per-run maxima (bmax): a wave whose 64 reads share a run keeps the run's
+    // max in a register and flushes it (one wave-reduced atomic) when the run
+    // changes; a wave straddling two runs flushes per lane
+    const uint64_t bq = b.bucket_reads ? b.bucket_reads : ~0ull;
+    uint32_t cur = ~0u, bm = 0;
+    for (uint64_t r0 = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); r0 < n; r0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t r = r0 + (threadIdx.x & 63u);
+        uint32_t len = 0;
+        if (r < n) {
+            const uint64_t j = ph + 4 * r;
+            const uint64_t k = ascii ? j : b.vline[j];
+            uint32_t st, en;
+            line_bounds(b, k, st, en);
+            len = en - st;
+            if (len > b.stride) tl = min(tl, v0 + j + 1);
+            mn = min(mn, len);
+            mx = max(mx, len);
+            bases += len;
+        }
+        const uint64_t rl = min(r0 + 63, n - 1);
+        const uint32_t k0 = (uint32_t)min<uint64_t>(r0 / bq, kLenBuckets - 1);
+        const uint32_t k1 = (uint32_t)min<uint64_t>(rl / bq, kLenBuckets - 1);
+        if (k0 != k1) {  // wave-uniform: this wave's reads cross a run boundary
+            if (r < n) atomicMax(&o->bmax[(uint32_t)min<uint64_t>(r / bq, kLenBuckets - 1)], len);
+            continue;
+        }
+        if (k0 != cur) {
+            if (cur != ~0u) {
+                const uint32_t w = wave_max_u32(bm);
+                if ((threadIdx.x & 63) == 0) atomicMax(&o->bmax[cur], w);
+            }
+            cur = k0;
+            bm = 0;
+        }
+        bm = max(bm, len);
+    }
+    if (cur != ~0u) {
+        const uint32_t w = wave_max_u32(bm);
+        if ((threadIdx.x & 63) == 0) atomicMax(&o->bmax[cur], w);
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {

@@ -123,6 +123,7 @@ class GpuFastqReader:
         """-> DevReadsT, or with host=True (seqs u8[n, stride], lens u16[n][, pos i64[n]])."""
         d = DevReadsT()
         check(lib().msw_gfastq_next(self._h, None, ctypes.byref(d)))
+        self.last = d  # the batch's descriptor (n, first_read, min_len / max_len bounds)
         if not host:
             return d
         n = int(d.n)

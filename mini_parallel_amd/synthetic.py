@@ -202,15 +202,17 @@ def bgzf_compress(data: bytes, level: int = 1, strategy: int = 0, block: int = 0
     return b"".join(out)
 
 
-def _lane_reads(g, k, reads_per_file, read_len, win_factor, seed):
+def _lane_reads(g, k, reads_per_file, read_len, win_factor, seed, segment=0):
     """The reads of lane file k of a write_wgs_dataset run and their window
     positions (every read gets a window of the genome: unrelated reads, pos
     -1 in make_pairs, are paired with a random window), plus the rng the
-    writer continues with for the quality strings."""
+    writer continues with for the quality strings.  ``segment`` > 0: the
+    segment-th run of reads of a file written in segments
+    (write_lane_file_segmented; segment 0 is the unsegmented file)."""
     genome_bases = int(g.shape[0])
-    b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k, genome_arr=g,
+    b = make_pairs(reads_per_file, read_len, win_factor, seed=seed * 1000 + k + 1_000_003 * segment, genome_arr=g,
                    read_stride=(read_len + 16 + 15) // 16 * 16)
-    rng = np.random.default_rng([seed, k])
+    rng = np.random.default_rng([seed, k] if segment == 0 else [seed, k, segment])
     span = genome_bases - int(b.win_len.max())
     pos = np.where(b.pos >= 0, np.minimum(b.pos, span), rng.integers(0, span, b.n_pairs))
     return b, pos, rng
@@ -239,13 +241,9 @@ def lane_file_batch(k: int, reads_per_file: int, read_len: int = 150, win_factor
     return _with_windows(g, b, pos)
 
 
-def _write_lane_file(job):
-    """One lane file of write_wgs_dataset (a process-pool job)."""
-    import gzip
-    (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep, bgzf, qual) = job
-    b, pos, rng = _lane_reads(g, k, reads_per_file, read_len, win_factor, seed)
+def _lane_records(b, pos, rng, tag: bytes, lane: int, qual: str, first: int = 0) -> bytes:
+    """FASTQ text of one run of lane reads (read ids from ``first``)."""
     rl = b.read_len.astype(np.int64)
-    tag = sample.encode()
     if qual == "I":
         q = b"I" * int(rl.max() if b.n_pairs else 0)
         quals = [q[:rl[i]] for i in range(b.n_pairs)]
@@ -262,17 +260,45 @@ def _write_lane_file(job):
         ends = np.cumsum(rl)
         raw = qb.tobytes()
         quals = [raw[int(e - m):int(e)] for e, m in zip(ends, rl)]
-    recs = [b"@%s:%d:%d pos=%d\n%s\n+\n%s\n" % (tag, lane, i, int(pos[i]), b.reads[i, :rl[i]].tobytes(),
-                                                  quals[i]) for i in range(b.n_pairs)]
+    return b"".join([b"@%s:%d:%d pos=%d\n%s\n+\n%s\n" % (tag, lane, first + i, int(pos[i]),
+                                                          b.reads[i, :rl[i]].tobytes(), quals[i])
+                     for i in range(b.n_pairs)])
+
+
+def _write_lane_file(job):
+    """One lane file of write_wgs_dataset (a process-pool job)."""
+    import gzip
+    (g, name, sample, lane, k, reads_per_file, read_len, win_factor, seed, compresslevel, keep, bgzf, qual) = job
+    b, pos, rng = _lane_reads(g, k, reads_per_file, read_len, win_factor, seed)
+    text = _lane_records(b, pos, rng, sample.encode(), lane, qual)
     if bgzf:
         with open(name, "wb") as f:
-            f.write(bgzf_compress(b"".join(recs), compresslevel))
+            f.write(bgzf_compress(text, compresslevel))
     else:
         with gzip.open(name, "wb", compresslevel=compresslevel) as f:
-            f.write(b"".join(recs))
+            f.write(text)
     if not keep:
         return None
     return _with_windows(g, b, pos)
+
+
+def write_lane_file_segmented(job) -> int:
+    """A BGZF lane file of ``reads_per_file`` reads written in segments of
+    ``segment`` reads (bounded memory for full-size lane files: BASELINE
+    config 4 is ~50 M reads per lane), each segment its own seeded run of
+    reads, appended as whole BGZF members; the EOF block last.  Returns the
+    file's size.  (A process-pool job: tools/c4_full.py.)"""
+    (g, name, sample, lane, k, reads_per_file, segment, read_len, win_factor, seed, compresslevel, qual) = job
+    done = 0
+    with open(name, "wb") as f:
+        for seg in range((reads_per_file + segment - 1) // segment):
+            n = min(segment, reads_per_file - done)
+            b, pos, rng = _lane_reads(g, k, n, read_len, win_factor, seed, segment=seg)
+            f.write(bgzf_compress(_lane_records(b, pos, rng, sample.encode(), lane, qual, first=done), compresslevel,
+                                  eof_block=False))
+            done += n
+        f.write(BGZF_EOF)
+        return f.tell()
 
 
 def write_wgs_dataset(out_dir: str, sample: str = "SYN", lanes: int = 2, reads_per_lane: int = 2,

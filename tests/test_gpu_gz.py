@@ -343,3 +343,32 @@ def test_reader_wide_slabs(gpu_ctx, tmp_path, stride, lo, hi):
     p = tmp_path / "wide.fastq.gz"
     p.write_bytes(bgzf_compress(b"".join(recs), 6, block=20000))
     assert assert_reader_parity(gpu_ctx, str(p), stride=stride, max_reads=700) == 1500
+
+
+@pytest.mark.parametrize("max_reads,group", [(64, 1), (7, 4)])
+def test_reader_batch_length_bound(gpu_ctx, tmp_path, max_reads, group):
+    """Each batch's max_len (the bound the scorer picks its kernel by) is the
+    longest read of its own run of batches, not of the whole span: two
+    300-base reads among 20..150-base ones widen only their runs' batches.
+    A run is `group` batches when a span holds more than 256 batches."""
+    rng = np.random.default_rng(77)
+    n, outliers = 12000, (500, 7000)
+    recs = []
+    for i in range(n):
+        m = 300 if i in outliers else int(rng.integers(20, 151))
+        seq = bytes(np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, m)])
+        recs.append(b"@r%d\n" % i + seq + b"\n+\n" + b"I" * m + b"\n")
+    p = tmp_path / "bound.fastq.gz"
+    p.write_bytes(bgzf_compress(b"".join(recs), 6, block=20000))
+    wide, got = 0, 0
+    with GpuFastqReader(gpu_ctx, str(p), 512, max_reads, span_bytes=1 << 20) as g:
+        while True:
+            _, ln = g.next_batch()
+            if len(ln) == 0:
+                break
+            d = g.last
+            assert d.max_len >= int(ln.max()) and d.min_len <= int(ln.min())
+            wide += d.max_len >= 300
+            got += len(ln)
+    assert got == n
+    assert 2 <= wide <= 2 * group

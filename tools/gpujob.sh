@@ -10,6 +10,10 @@
 #   e2e[=ENVSETS]          tools/wgs_e2e.py over the config-4-shape BGZF set (16 x 2 M reads, binned, level 6);
 #                          ENVSETS as wgs_e2e.py --extra-env (default MSW_GPU_INFLATE=1)
 #   longbench              tools/long_bench.py
+#   sys                    df / free / CPU quota of the box (disk and memory for the full-size config-4 set)
+#   c4full[=READS]         tools/c4_full.py: BASELINE config 4 at full size (16 files x READS, default 25 M)
+#   traffic                tools/traffic_split.sh (FETCH_SIZE of the probe builds, configs 2 and 5)
+#   hostfeed               tools/host_feed.sh (config-4 host feed: copy rates, CLI runs with setup traced)
 # Example: gpurun --timeout 1200 -- bash tools/gpujob.sh r03a tests smoke bench prof
 set -euo pipefail
 T=${1:?tag}
@@ -45,6 +49,17 @@ for step in "$@"; do
     longbench)
       timeout -k 10 300 python3 tools/long_bench.py > "$OUT/long_bench.jsonl" 2> "$OUT/long_bench.err"
       echo "longbench ok" ;;
+    sys)
+      { df -h /tmp /dev/shm; free -g; nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null || true; } > "$OUT/sys.txt" 2>&1
+      cat "$OUT/sys.txt" ;;
+    c4full)
+      timeout -k 10 1100 python3 tools/c4_full.py --reads-per-file "${arg:-25000000}" \
+        --out "$OUT/config4_full.jsonl" > "$OUT/c4full.log" 2>&1
+      tail -5 "$OUT/c4full.log" ;;
+    traffic)
+      bash tools/traffic_split.sh "$T/traffic" ;;
+    hostfeed)
+      bash tools/host_feed.sh "$T/hostfeed" ;;
     *)
       echo "unknown step $name" >&2; exit 2 ;;
   esac
