@@ -224,7 +224,10 @@ def test_cli_full_wgs_under_asan_on_gpu(tmp_path, oracle, gpu_inflate):
     env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "2",
            "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "700", "WGS_RUN_ID": "asan",
            "MSW_GPU_INFLATE": gpu_inflate, "MSW_GFASTQ_BATCH": "500", "MSW_GFASTQ_SPAN_MB": "1",
-           "MSW_DEVICES": "0,0", "ASAN_OPTIONS": "halt_on_error=1:detect_leaks=0:exitcode=86"}
+           "MSW_DEVICES": "0,0",
+           # no quarantine: the sanitizer runtime tracks HSA allocations too and
+           # must not recycle one after the HIP runtime has unloaded at exit
+           "ASAN_OPTIONS": "halt_on_error=1:detect_leaks=0:exitcode=86:quarantine_size_mb=0"}
     (tmp_path / "scores").mkdir()
     r = run(CLI, ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
                   "--num-gpus", "2", "--checkpoint-dir", tmp_path, "--json", tmp_path / "rec.json",
