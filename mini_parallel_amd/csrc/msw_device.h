@@ -1154,12 +1154,35 @@ __device__ __forceinline__ void trace_end(const SwParams& p, const WaveClock& w,
     }
 }
 
+// Blocks are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+// one; MI355X_MICROARCH.md, workgroup dispatch), each XCD with its own L2.
+// Adjacent blocks score adjacent pairs, whose row ends and length / order
+// entries share cache lines, so the identity map has up to 8 L2s fetch each
+// such line.  This (bijective) map gives each run of G consecutive logical
+// blocks to one XCD, within full windows of 8G blocks (a tail keeps the
+// identity); dispatch order moves by < 8G blocks, so heaviest-first grids
+// stay heaviest first.  Speed only (traffic), never correctness.
+template <uint32_t G>
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+#ifdef MSW_NO_XCD_REMAP  // A/B builds (tools/build_variant.sh)
+    return b;
+#endif
+    constexpr uint32_t span = 8u * G;
+    const uint32_t base = b - b % span;
+    if (base + span > nb) return b;
+    const uint32_t r = b - base;
+    return base + (r % 8u) * G + r / 8u;
+}
+
 // One layout for the whole grid.
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
 __global__ __launch_bounds__(64) void sw_kernel(SwParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const WaveClock wc = trace_begin(p);
     uint64_t t_loop = 0;
+    // identity block order: the XCD-grouped map below cut config 2's fetched
+    // bytes 5.36 -> 4.99 MB per launch but slowed it 46.2 -> 50.2 us
+    // (profiles/r03/traffic/xcd_remap_ab.jsonl); kept for the bucketed grid
     const bool fast = sw_body<KR, AFFINE, COORDS, SPLIT>(p, blockIdx.x, lds, t_loop);
     trace_end(p, wc, fast, SPLIT, KR, t_loop);
 }
@@ -1208,9 +1231,10 @@ __device__ __forceinline__ void multi_body(const SwParams& q, uint32_t blk, uint
 template <bool AFFINE, bool COORDS, bool WIDE = false>
 __global__ __launch_bounds__(64) void sw_multi_kernel(SwParams p, MultiTable t) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t lb = xcd_block<4>(blockIdx.x, gridDim.x);
     uint32_t b = 0;
-    while (b + 1 < t.n_buckets && blockIdx.x >= t.block_end[b]) ++b;
-    const uint32_t blk = blockIdx.x - (b ? t.block_end[b - 1] : 0u);
+    while (b + 1 < t.n_buckets && lb >= t.block_end[b]) ++b;
+    const uint32_t blk = lb - (b ? t.block_end[b - 1] : 0u);
     SwParams q = p;
     q.order = p.order + t.slot_begin[b];
     q.out_slot_base = p.out_slot_base + t.slot_begin[b];

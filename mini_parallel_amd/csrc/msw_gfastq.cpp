@@ -335,6 +335,7 @@ struct msw_gfastq {
 
     uint64_t span_reads = 0, span_done = 0, next_first = 0;
     uint32_t span_min = 0, span_max = 0;
+    uint64_t spans = 0;                     // spans parsed over the reader's life (all files)
     uint64_t bucket_reads = 1;              // reads per span_bmax entry
     uint32_t span_bmax[msw::kLenBuckets] = {};
     int failed = 0;  // sticky error code
@@ -516,6 +517,14 @@ int to_copied(msw_gfastq* g) {
     return fill_compressed(g, g->hc_cap);
 }
 
+uint64_t first_span_bytes() {
+    static const uint64_t v = [] {
+        const char* e = getenv("MSW_GFASTQ_FIRST_SPAN_MB");
+        return (e && atoll(e) > 0 ? (uint64_t)atoll(e) : 0ull) << 20;
+    }();
+    return v;
+}
+
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -534,9 +543,16 @@ int next_span(msw_gfastq* g) {
     g->mem.clear();
     size_t used = 0;
     uint64_t obytes = 0;
+    // MSW_GFASTQ_FIRST_SPAN_MB: a shorter first span for the reader (scoring
+    // starts sooner).  Measured slower, off by default: 256 MB first spans
+    // 99-102 vs 104-105 M reads/s over 16 files, 67-69 vs 76 M over 2 files
+    // (profiles/r03/e2e/first_span_ab.jsonl) -- fewer members per inflate
+    // launch cost more than the earlier start wins.
+    const uint64_t cap = g->spans == 0 && first_span_bytes() ? std::min<uint64_t>(g->span, first_span_bytes())
+                                                              : g->span;
     for (;;) {
-        if ((rc = index_members(g->hc, g->hc_len, kCarry, g->span, g->in_cap, g->mem, &used, &obytes))) return rc;
-        const bool full = obytes + 65536 > g->span || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
+        if ((rc = index_members(g->hc, g->hc_len, kCarry, cap, g->in_cap, g->mem, &used, &obytes))) return rc;
+        const bool full = obytes + 65536 > cap || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
         if (full) break;
         g->mem.clear();
         if ((rc = fill_compressed(g, g->hc_len + kReadPiece))) return rc;
@@ -647,6 +663,7 @@ int next_span(msw_gfastq* g) {
     g->at_eof = last;
     g->span_reads = o.reads;
     g->span_done = 0;
+    ++g->spans;
     g->span_min = o.min_len;
     g->span_max = o.max_len;
     g->bucket_reads = b.bucket_reads;
@@ -778,6 +795,12 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     g->in_cap = (size_t)(std::max<uint64_t>(g->span / 2, 16u << 20) + kReadPiece + (1u << 20));
     if (hipHostMalloc((void**)&g->h_out, sizeof(msw::ParseOut), hipHostMallocDefault) != hipSuccess)
         return bail(set_error(MSW_E_NOMEM, "hipHostMalloc failed (GPU lane reader staging)"));
+    {
+        // copied mode asked for up front: its pinned staging now, with the
+        // other buffers (~85 ms per 512 MB), not at the first file's read
+        const char* nm = getenv("MSW_GZ_NO_MAP");
+        if (nm && atoi(nm) != 0 && (rc = ensure_stage(g))) return bail(rc);
+    }
     const size_t ob = (size_t)(kCarry + g->span + kPad);
     for (int i = 0; i < 2; ++i) {
         if (hipMalloc((void**)&g->dout[i], ob) != hipSuccess ||

@@ -12,6 +12,8 @@
 #   longbench              tools/long_bench.py
 #   sys                    df / free / CPU quota of the box (disk and memory for the full-size config-4 set)
 #   c4full[=READS]         tools/c4_full.py: BASELINE config 4 at full size (16 files x READS, default 25 M)
+#   ab=VARIANT             bench configs 2 / 3 / 5 (kernel-only), in-tree build vs tools/_variants/libmsw_VARIANT.so,
+#                          alternating, 3 rounds -> gpurun_out/TAG/ab_VARIANT.jsonl
 #   traffic                tools/traffic_split.sh (FETCH_SIZE of the probe builds, configs 2 and 5)
 #   hostfeed               tools/host_feed.sh (config-4 host feed: copy rates, CLI runs with setup traced)
 # Example: gpurun --timeout 1200 -- bash tools/gpujob.sh r03a tests smoke bench prof
@@ -56,6 +58,17 @@ for step in "$@"; do
       timeout -k 10 1100 python3 tools/c4_full.py --reads-per-file "${arg:-25000000}" \
         --out "$OUT/config4_full.jsonl" > "$OUT/c4full.log" 2>&1
       tail -5 "$OUT/c4full.log" ;;
+    ab)
+      for rep in 1 2 3; do
+        for lib in "" "$PWD/tools/_variants/libmsw_$arg.so"; do
+          for cfg in 2 3 5; do
+            MSW_LIB_PATH=$lib timeout -k 10 300 python3 bench.py --config $cfg --steps 50 --warmup 5 --cpu-seconds 0 \
+              --no-pcie --extra-configs none > "$OUT/ab_tmp.json" 2>> "$OUT/ab.err"
+            python3 -c "import json,sys; d=json.load(open('$OUT/ab_tmp.json')); print(json.dumps({'lib': '${lib:-in-tree}', 'config': $cfg, 'rep': $rep, 'value': d['value'], 'avg_launch_ms': d['roofline']['avg_launch_ms'], 'bit_exact': (d.get('parity') or {}).get('bit_exact')}))" >> "$OUT/ab_$arg.jsonl"
+          done
+        done
+      done
+      cat "$OUT/ab_$arg.jsonl" ;;
     traffic)
       bash tools/traffic_split.sh "$T/traffic" ;;
     hostfeed)
