@@ -514,27 +514,30 @@ struct WinRound {
 };
 
 template <bool SPLIT>
-__device__ __forceinline__ void load_round(const SwParams& p, uint32_t pa, uint32_t pb, int k0, int lg, int G,
+__device__ __forceinline__ void load_round(const SwParams& p, const PairMeta& q, int k0, int lg, int G,
                                            WinRound& w) {
-    const uint8_t* wa = p.wins + (uint64_t)pa * p.win_stride;
-    const uint8_t* wb = p.wins + (uint64_t)pb * p.win_stride;
-    // last chunk to load: the row's end or the stream's (the launch's longest
-    // window), whichever comes first -- lanes past it re-load that chunk (the
-    // same line, coalesced) instead of touching a line past the windows
+    const uint8_t* wa = p.wins + (uint64_t)q.pa * p.win_stride;
+    const uint8_t* wb = p.wins + (uint64_t)q.pb * p.win_stride;
+    // last chunk to load per pair: the end of ITS window (not the launch's
+    // longest, which a length bucket's short windows would over-read by up to
+    // a 128-byte line each), and never past the row or the stream -- lanes
+    // past it re-load that chunk (the same line, coalesced)
     const int top = min((int)(p.win_stride >> 4), (int)((p.lds_stride - kLead) >> 4)) - 1;
+    const int top_a = max(min(top, ((q.na + 15) >> 4) - 1), 0);
+    const int top_b = max(min(top, ((q.nb + 15) >> 4) - 1), 0);
     const int last = (int)p.win_stride - 1;
 #pragma unroll
     for (int u = 0; u < kRound; ++u) {
         // clamped chunk index: always a legal load; columns past the window are masked
-        const int k = min(k0 + u * G + lg, top);
+        const int k = k0 + u * G + lg;
 #if MSW_PROBE_NO_WIN
-        w.a[u] = w.b[u] = make_uint4(0x03020100u + k, 0x01000302u, 0x02010003u, 0x00030201u ^ (uint32_t)pa);
+        w.a[u] = w.b[u] = make_uint4(0x03020100u + min(k, top), 0x01000302u, 0x02010003u, 0x00030201u ^ q.pa);
         w.prev[u] = 0;
-        (void)wa; (void)wb; (void)last;
+        (void)wa; (void)wb; (void)last; (void)top_a; (void)top_b;
 #else
-        w.a[u] = *reinterpret_cast<const uint4*>(wa + 16 * k);
-        if constexpr (SPLIT) w.prev[u] = wa[min(max(16 * (k0 + u * G + lg) - 1, 0), last)];
-        else w.b[u] = *reinterpret_cast<const uint4*>(wb + 16 * k);
+        w.a[u] = *reinterpret_cast<const uint4*>(wa + 16 * min(k, top_a));
+        if constexpr (SPLIT) w.prev[u] = wa[min(max(16 * k - 1, 0), last)];
+        else w.b[u] = *reinterpret_cast<const uint4*>(wb + 16 * min(k, top_b));
 #endif
     }
 }
@@ -702,7 +705,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     const bool try_fast = p.f16_ok && p.win_vec;
     WinRound w0;
 #if MSW_EARLY_WIN_LOADS
-    if (try_fast) load_round<SPLIT>(p, q.pa, q.pb, 0, lg, G, w0);
+    if (try_fast) load_round<SPLIT>(p, q, 0, lg, G, w0);
 #endif
     const int skew = SPLIT ? 2 * (G - 1) + 1 : G - 1;
     // wavefront steps, rounded up to a multiple of the steps per iteration
@@ -712,7 +715,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     const int steps = (wave_max_nonneg(max(q.na, q.nb)) + skew + kUnroll - 1) & ~(kUnroll - 1);
     uint32_t* stream = lds + g * p.lds_stride;
 #if !MSW_EARLY_WIN_LOADS
-    if (try_fast) load_round<SPLIT>(p, q.pa, q.pb, 0, lg, G, w0);
+    if (try_fast) load_round<SPLIT>(p, q, 0, lg, G, w0);
 #endif
     uint32_t rc[KR];
     read_codes<KR, SPLIT>(p, q, lg, rb_a, rb_b, rc);
@@ -725,7 +728,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
             bad = sel_round<SPLIT>(q, stream, 0, nch, lg, G, w0);
             for (int k0 = kRound * G; k0 < nch; k0 += kRound * G) {  // windows past 16 kRound G columns
                 WinRound w;
-                load_round<SPLIT>(p, q.pa, q.pb, k0, lg, G, w);
+                load_round<SPLIT>(p, q, k0, lg, G, w);
                 bad |= sel_round<SPLIT>(q, stream, k0, nch, lg, G, w);
             }
         }
