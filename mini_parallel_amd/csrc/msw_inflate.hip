@@ -53,6 +53,10 @@ constexpr int kDefaultRingKb = 2;  // best measured throughput (tools/inflate_be
 #else
 #define GZP(i, v) ((void)0)
 #endif
+// MSW_GZ_SPEC=0 builds the one-token-at-a-time Huffman loop (A/B variant)
+#ifndef MSW_GZ_SPEC
+#define MSW_GZ_SPEC 1
+#endif
 
 constexpr uint32_t kChunk = 256;  // flush unit: 64 lanes x 4 bytes
 
@@ -569,6 +573,217 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 return L | kFastMatch | ((L + x) << 8) | (x << 16) | (b << 23);
             };
             if (!br.refill()) { err = GZ_E_TRUNC; break; }
+#if MSW_GZ_SPEC
+            // Speculative window decode.  The serial part of inflate is only
+            // "where does the next token start"; everything else about a token
+            // (table lookups, length and distance with their extra bits) is a
+            // function of its start bit.  So lane L decodes the token that
+            // WOULD start at bit P + L of the stream (64 candidate starts, all
+            // on the VALU, both table lookups per lane), packs it into one
+            // dword, and the wave then walks the chain -- token at offset k,
+            // next at k + its bits -- with one v_readlane per token, doing the
+            // ring writes / copies in order.  A window covers 64 bits (~4
+            // tokens of FASTQ); the scalar unit, which bounds the one-token-at-
+            // a-time loop (~50 SALU per match token), only runs the walk.
+            // Tokens the window does not resolve -- codes longer than the fast
+            // tables, end of block, invalid codes, a distance too far back, and
+            // the last 112 bits of the member -- go to the scalar step below
+            // (one token, the exact bit reader and error rules of the loop it
+            // replaces), after which the window resumes at its end.
+            //   info bits: [31] simple, [30] match;
+            //   match:   [5:0] bits, [14:6] length, [29:15] distance - 1
+            //   literal: [3:0] bits, [5:4] count (1..3), [29:6] the bytes
+            auto copy_match = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
+                if (dist + len <= kRing) {
+                    const float rd = __builtin_amdgcn_rcpf((float)dist);
+                    uint32_t j0 = 0;
+                    do {
+                        const uint32_t j = j0 + lane;
+                        int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
+                        r += r < 0 ? (int32_t)dist : 0;
+                        r -= r >= (int32_t)dist ? (int32_t)dist : 0;
+                        const uint32_t on = 0u - (uint32_t)(j < len);
+                        const uint32_t src = ((opos - dist + (uint32_t)r) & kRingMask) & on;
+                        const uint32_t dsti = ((opos + j) & kRingMask) & on;
+                        const uint8_t v = ring[src | (dummy & ~on)];
+                        ring[dsti | (dummy & ~on)] = v;
+                        j0 += 64;
+                    } while (j0 < len);
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
+                    uint32_t j0 = 0;
+                    do {
+                        const uint32_t j = j0 + lane;
+                        const bool on = j < len;
+                        const uint64_t q = mem.ooff + (uint64_t)(opos - dist + (on ? j : 0u));
+                        const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
+                        ring[on ? ((opos + j) & kRingMask) : dummy] = (uint8_t)(w >> (8u * (uint32_t)(q & 3)));
+                        j0 += 64;
+                    } while (j0 < len);
+                }
+            };
+            const uint32_t lit_shift6 = 6u + 8u * min(lane, 2u);
+            const uint64_t cend = mem.coff + mem.clen;
+            const uint32_t ew = (uint32_t)(cend >> 2), eb = 8u * (uint32_t)(cend & 3u);
+            // stream position (dword, bit) of the bit reader: wi * 32 - bcnt
+            uint32_t pw = br.wi - (br.bcnt >> 5) - ((br.bcnt & 31u) ? 1u : 0u);
+            uint32_t pb = (32u - (br.bcnt & 31u)) & 31u;
+            uint32_t bad = 0;
+            for (;;) {
+                const int32_t remain = (int32_t)(ew - pw) * 32 + (int32_t)eb - (int32_t)pb;
+                uint32_t k = 64;
+                if (remain >= 112) {  // every candidate token ends inside the member
+                    if (pw - br.wbase > 59u) {
+                        br.wbase = pw;
+                        br.cur = br.src[pw + lane];
+                    }
+                    const int r0 = (int)(pw - br.wbase);
+                    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0);
+                    const uint32_t d1 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 1);
+                    const uint32_t d2 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 2);
+                    const uint32_t d3 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 3);
+                    const uint32_t d4 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 4);
+                    const uint32_t o = pb + lane, jw = o >> 5, bs = o & 31u;
+                    const uint32_t A = jw == 0 ? d0 : (jw == 1 ? d1 : d2);
+                    const uint32_t B = jw == 0 ? d1 : (jw == 1 ? d2 : d3);
+                    const uint32_t C = jw == 0 ? d2 : (jw == 1 ? d3 : d4);
+                    const uint32_t x = __builtin_amdgcn_alignbit(B, A, bs);  // stream bits [P + lane, +32)
+                    const uint32_t y = __builtin_amdgcn_alignbit(C, B, bs);  // [+32, +64)
+                    const uint32_t e = S.u.fast_ll[x & ((1u << kFastBits) - 1u)];
+                    const uint32_t c = (e >> 8) & 63u;                      // a length's code + extra bits
+                    const uint32_t z = __builtin_amdgcn_alignbit(y, x, c);  // the distance's bits
+                    const uint32_t di = z & ((1u << kFastDBits) - 1u);
+                    const uint32_t ed = S.fast_d[di], dbase = S.fast_dbase[di];
+                    const uint32_t len = (e >> 23) + __builtin_amdgcn_ubfe(x, e & 31u, (e >> 16) & 127u);
+                    const uint32_t dist = dbase + __builtin_amdgcn_ubfe(z, ed & 31u, (ed >> 16) & 31u);
+                    const uint32_t tm = c + ((ed >> 8) & 31u);
+                    const uint32_t lit = 0x80000000u | (e & 15u) | (((e >> 4) & 3u) << 4) | ((e >> 8) << 6);
+                    const uint32_t mat = 0xC0000000u | tm | (len << 6) | ((dist - 1u) << 15);
+                    const uint32_t m_lit = 0u - (uint32_t)((e & 0x30u) != 0);
+                    // a match resolves here if both codes were in the fast tables
+                    // and its distance reaches no further back than the output
+                    // so far (opos only grows during the walk; a match that fails
+                    // this but not the exact test goes to the scalar step, which
+                    // copies it)
+                    const uint32_t m_mat = 0u - (uint32_t)((e & kFastMatch) != 0 && (ed & kFastDLong) == 0 && dist <= opos);
+                    const uint32_t info = (lit & m_lit) | (mat & m_mat & ~m_lit);
+                    GZP(7, 1);
+                    // the walk: one exit (k past the window); a token the window
+                    // cannot take, or an overrun, ends it by pushing k out of range
+                    k = 0;
+                    uint32_t kstop = 0;
+                    do {
+                        const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k);
+                        if (s & 0x40000000u) {
+                            const uint32_t ln = (s >> 6) & 511u, ds = ((s >> 15) & 0x7FFFu) + 1u;
+                            GZP(5, 1);
+                            copy_match(ln, ds);
+                            opos += ln;
+                            k += s & 63u;
+                        } else if ((int32_t)s < 0) {
+                            GZP(2, 1);
+                            const uint32_t nlit = (s >> 4) & 3u;
+                            ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(s >> lit_shift6);
+                            opos += nlit;
+                            k += s & 15u;
+                        } else {
+                            kstop = k;  // not a simple token: the scalar step takes it
+                            k = 0x10000u;
+                        }
+                        if (__builtin_expect(opos - flushed >= kChunk, 0)) {
+                            if (opos > isize) {
+                                bad = GZ_E_OVERRUN;
+                                kstop = k;
+                                k = 0x10000u;
+                            } else {
+                                do { flush_chunk(flushed); flushed += kChunk; } while (opos - flushed >= kChunk);
+                            }
+                        }
+                    } while (k < 64);
+                    if (k == 0x10000u) k = kstop;
+                    pb += k;
+                    pw += pb >> 5;
+                    pb &= 31u;
+                    if (bad) {
+                        br.wi = pw + 1;  // the position for the truncation test at the end
+                        br.bcnt = 32u - pb;
+                        break;
+                    }
+                    if (k >= 64) continue;
+                }
+                // Scalar step: one token from (pw, pb) with the bit reader.
+                GZP(4, 1);
+                if (pw - br.wbase > 62u) {
+                    br.wbase = min(pw, br.wmax);
+                    br.cur = br.src[br.wbase + lane];
+                }
+                {
+                    const uint32_t q = pw - br.wbase;
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, (int)(q & 63u));
+                    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, (int)((q + 1u) & 63u));
+                    br.bb = ((((uint64_t)hi) << 32) | lo) >> pb;
+                    br.bcnt = 64u - pb;
+                    br.wi = pw + 2u;
+                }
+                uint32_t e = __builtin_amdgcn_readfirstlane(lookup());
+                if (e & kFastLong) e = slow_ll();
+                bool eob = false;
+                if (e & 0x30u) {
+                    const uint32_t nlit = (e >> 4) & 3u;
+                    br.drop(e & 15u);
+                    if (br.bcnt < 32) br.refill_fast();
+                    ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
+                    opos += nlit;
+                    if (opos - flushed >= kChunk && !flush_to()) bad = GZ_E_OVERRUN;
+                } else if (!(e & kFastMatch)) {  // end of block, or no code of this set
+                    if (e & kFastBadE) bad = GZ_E_SYMBOL;
+                    else { br.drop(e & 15u); eob = true; }
+                } else {
+                    const uint32_t len = (e >> 23) + sbfe((uint32_t)br.bb, e);
+                    br.drop((e >> 8) & 63u);
+                    if (br.bcnt < 32) br.refill_fast();
+                    const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
+                    uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
+                    uint32_t dbase = __builtin_amdgcn_readfirstlane(S.fast_dbase[di]);
+                    if (ed & kFastDLong) {
+                        const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;
+                        const uint64_t m = __ballot(r < lim_d);
+                        uint32_t L = 0, d = 31;
+                        if (m) {
+                            L = (uint32_t)__builtin_ctzll(m);
+                            const int32_t base = __builtin_amdgcn_readlane(bas_d, (int)L);
+                            d = __builtin_amdgcn_readfirstlane((uint32_t)S.sym_d[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
+                        }
+                        ed = 0;
+                        dbase = 0xFFFFFFFFu;
+                        if (d > 29) {
+                            bad = GZ_E_SYMBOL;
+                        } else {
+                            uint32_t xb;
+                            dbase = dist_base(d, xb);
+                            ed = L | ((L + xb) << 8) | (xb << 16);
+                        }
+                    }
+                    const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);
+                    br.drop((ed >> 8) & 31u);
+                    if (br.bcnt < 32) br.refill_fast();
+                    if (dist > opos) {
+                        bad = bad ? bad : (uint32_t)GZ_E_DIST;
+                    } else {
+                        copy_match(len, dist);
+                        opos += len;
+                        if (opos - flushed >= kChunk && !flush_to()) bad = GZ_E_OVERRUN;
+                    }
+                }
+                if (bad || eob) break;
+                pw = br.wi - (br.bcnt >> 5) - ((br.bcnt & 31u) ? 1u : 0u);
+                pb = (32u - (br.bcnt & 31u)) & 31u;
+            }
+            if (bad) {
+                err = bad;
+                break;
+            }
+#else
             uint32_t ev = lookup();
             // One exit: every failure lands in `bad` (the literal run masks its
             // next entry to "not a literal", the match path checks once before
@@ -697,6 +912,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 err = bad;
                 break;
             }
+#endif
         }
         // a decode that ran into the bytes after the member (its last refills
         // merge them unchecked) failed because the member is truncated

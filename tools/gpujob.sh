@@ -14,6 +14,8 @@
 #   c4full[=READS]         tools/c4_full.py: BASELINE config 4 at full size (16 files x READS, default 25 M)
 #   ab=VARIANT             bench configs 2 / 3 / 5 (kernel-only), in-tree build vs tools/_variants/libmsw_VARIANT.so,
 #                          alternating, 3 rounds -> gpurun_out/TAG/ab_VARIANT.jsonl
+#   gzab=VARIANT           GPU inflate, in-tree build vs tools/_variants/libmsw_VARIANT.so, alternating, 3 rounds:
+#                          tools/inflate_bench.py at 16384 members (fastq, binned, level 6), MSW_GZ_TIMING kernel times
 #   traffic                tools/traffic_split.sh (FETCH_SIZE of the probe builds, configs 2 and 5)
 #   hostfeed               tools/host_feed.sh (config-4 host feed: copy rates, CLI runs with setup traced)
 # Example: gpurun --timeout 1200 -- bash tools/gpujob.sh r03a tests smoke bench prof
@@ -69,6 +71,15 @@ for step in "$@"; do
         done
       done
       cat "$OUT/ab_$arg.jsonl" ;;
+    gzab)
+      for rep in 1 2 3; do
+        for lib in "" "$PWD/tools/_variants/libmsw_$arg.so"; do
+          echo "== lib ${lib:-in-tree} rep $rep" >> "$OUT/gzab_$arg.log"
+          MSW_LIB_PATH=$lib MSW_GZ_TIMING=1 timeout -k 10 300 python3 tools/inflate_bench.py --members 16384 \
+            >> "$OUT/gzab_$arg.log" 2>&1
+        done
+      done
+      grep -E "==|members|inflate" "$OUT/gzab_$arg.log" | tail -40 ;;
     traffic)
       bash tools/traffic_split.sh "$T/traffic" ;;
     hostfeed)
