@@ -593,31 +593,37 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             //   info bits: [31] simple, [30] match;
             //   match:   [5:0] bits, [14:6] length, [29:15] distance - 1
             //   literal: [3:0] bits, [5:4] count (1..3), [29:6] the bytes
+            // Lanes past the match's end repeat its last byte (the same value to
+            // the same ring address), so no lane needs a select or a dummy byte.
             auto copy_match = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
+                const uint32_t last = len - 1u;
                 if (dist + len <= kRing) {
+                    // ring -> ring; byte j copies source byte j mod dist
+                    // (overlapping copies repeat the last `dist` bytes)
                     const float rd = __builtin_amdgcn_rcpf((float)dist);
+                    const uint32_t base = opos - dist;
                     uint32_t j0 = 0;
                     do {
-                        const uint32_t j = j0 + lane;
+                        const uint32_t j = min(j0 + lane, last);
                         int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
                         r += r < 0 ? (int32_t)dist : 0;
                         r -= r >= (int32_t)dist ? (int32_t)dist : 0;
-                        const uint32_t on = 0u - (uint32_t)(j < len);
-                        const uint32_t src = ((opos - dist + (uint32_t)r) & kRingMask) & on;
-                        const uint32_t dsti = ((opos + j) & kRingMask) & on;
-                        const uint8_t v = ring[src | (dummy & ~on)];
-                        ring[dsti | (dummy & ~on)] = v;
+                        const uint8_t v = ring[(base + (uint32_t)r) & kRingMask];
+                        ring[(opos + j) & kRingMask] = v;
                         j0 += 64;
                     } while (j0 < len);
                 } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
+                    // further back than the ring: the flushed output in L2 (the
+                    // source ends well before `flushed`), once the flush stores
+                    // have landed
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                    const uint64_t base = mem.ooff + (uint64_t)(opos - dist);
                     uint32_t j0 = 0;
                     do {
-                        const uint32_t j = j0 + lane;
-                        const bool on = j < len;
-                        const uint64_t q = mem.ooff + (uint64_t)(opos - dist + (on ? j : 0u));
+                        const uint32_t j = min(j0 + lane, last);
+                        const uint64_t q = base + j;
                         const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
-                        ring[on ? ((opos + j) & kRingMask) : dummy] = (uint8_t)(w >> (8u * (uint32_t)(q & 3)));
+                        ring[(opos + j) & kRingMask] = (uint8_t)(w >> (8u * (uint32_t)(q & 3)));
                         j0 += 64;
                     } while (j0 < len);
                 }
@@ -629,24 +635,25 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             uint32_t pw = br.wi - (br.bcnt >> 5) - ((br.bcnt & 31u) ? 1u : 0u);
             uint32_t pb = (32u - (br.bcnt & 31u)) & 31u;
             uint32_t bad = 0;
+            // the window runs while the member has >= 112 bits left at its start
+            // (remain = (ew - pw) * 32 + eb - pb >= 112 <=> pw <= pw_last): the
+            // last token of a window starts below bit 64 and takes <= 48 bits
+            const uint32_t pw_last = ew >= 4u ? ew - 4u : 0u;  // (4 * 32 + eb - pb >= 112 holds when eb >= pb - 16)
             for (;;) {
-                const int32_t remain = (int32_t)(ew - pw) * 32 + (int32_t)eb - (int32_t)pb;
                 uint32_t k = 64;
-                if (remain >= 112) {  // every candidate token ends inside the member
+                const bool room = pw < pw_last || (pw == pw_last && ew >= 4u && eb + 16u >= pb);
+                if (room) {  // every candidate token ends inside the member
                     if (pw - br.wbase > 59u) {
                         br.wbase = pw;
                         br.cur = br.src[pw + lane];
                     }
-                    const int r0 = (int)(pw - br.wbase);
-                    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0);
-                    const uint32_t d1 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 1);
-                    const uint32_t d2 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 2);
-                    const uint32_t d3 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 3);
-                    const uint32_t d4 = (uint32_t)__builtin_amdgcn_readlane((int)br.cur, r0 + 4);
-                    const uint32_t o = pb + lane, jw = o >> 5, bs = o & 31u;
-                    const uint32_t A = jw == 0 ? d0 : (jw == 1 ? d1 : d2);
-                    const uint32_t B = jw == 0 ? d1 : (jw == 1 ? d2 : d3);
-                    const uint32_t C = jw == 0 ? d2 : (jw == 1 ? d3 : d4);
+                    // lane L's stream bits from bit P + L: dwords j .. j + 2 of the
+                    // window, j = (pb + L) / 32, fetched from `cur` across lanes
+                    const uint32_t o = pb + lane, bs = o & 31u;
+                    const int a0 = (int)(((pw - br.wbase) + (o >> 5)) << 2);
+                    const uint32_t A = (uint32_t)__builtin_amdgcn_ds_bpermute(a0, (int)br.cur);
+                    const uint32_t B = (uint32_t)__builtin_amdgcn_ds_bpermute(a0 + 4, (int)br.cur);
+                    const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(a0 + 8, (int)br.cur);
                     const uint32_t x = __builtin_amdgcn_alignbit(B, A, bs);  // stream bits [P + lane, +32)
                     const uint32_t y = __builtin_amdgcn_alignbit(C, B, bs);  // [+32, +64)
                     const uint32_t e = S.u.fast_ll[x & ((1u << kFastBits) - 1u)];
