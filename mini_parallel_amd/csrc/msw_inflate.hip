@@ -595,11 +595,22 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             //   literal: [3:0] bits, [5:4] count (1..3), [29:6] the bytes
             // Lanes past the match's end repeat its last byte (the same value to
             // the same ring address), so no lane needs a select or a dummy byte.
-            auto copy_match = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
+            auto copy_near = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
                 const uint32_t last = len - 1u;
-                if (dist + len <= kRing) {
-                    // ring -> ring; byte j copies source byte j mod dist
-                    // (overlapping copies repeat the last `dist` bytes)
+                if (dist >= len) {
+                    // ring -> ring, source and destination apart: byte j from
+                    // byte j of the source (no modulo on the dependent path)
+                    const uint32_t base = opos - dist;
+                    uint32_t j0 = 0;
+                    do {
+                        const uint32_t j = min(j0 + lane, last);
+                        const uint8_t v = ring[(base + j) & kRingMask];
+                        ring[(opos + j) & kRingMask] = v;
+                        j0 += 64;
+                    } while (j0 < len);
+                } else {
+                    // overlapping (dist < len <= 258, so within the ring): byte j
+                    // copies source byte j mod dist (the last `dist` bytes repeat)
                     const float rd = __builtin_amdgcn_rcpf((float)dist);
                     const uint32_t base = opos - dist;
                     uint32_t j0 = 0;
@@ -612,7 +623,11 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                         ring[(opos + j) & kRingMask] = v;
                         j0 += 64;
                     } while (j0 < len);
-                } else {
+                }
+            };
+            auto copy_far = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
+                const uint32_t last = len - 1u;
+                {
                     // further back than the ring: the flushed output in L2 (the
                     // source ends well before `flushed`), once the flush stores
                     // have landed
@@ -627,6 +642,10 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                         j0 += 64;
                     } while (j0 < len);
                 }
+            };
+            auto copy_match = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
+                if (dist + len <= kRing) copy_near(len, dist);
+                else copy_far(len, dist);
             };
             const uint32_t lit_shift6 = 6u + 8u * min(lane, 2u);
             const uint64_t cend = mem.coff + mem.clen;
