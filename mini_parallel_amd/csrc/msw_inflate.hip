@@ -57,6 +57,10 @@ constexpr int kDefaultRingKb = 2;  // best measured throughput (tools/inflate_be
 #ifndef MSW_GZ_SPEC
 #define MSW_GZ_SPEC 1
 #endif
+// MSW_GZ_WPE=1: a window's output made lane-parallel (=0: the serial walk)
+#ifndef MSW_GZ_WPE
+#define MSW_GZ_WPE 1
+#endif
 
 constexpr uint32_t kChunk = 256;  // flush unit: 64 lanes x 4 bytes
 
@@ -359,6 +363,27 @@ __device__ __forceinline__ int decode_sym(Bits& br, uint32_t lim, int32_t bas, c
     const uint32_t idx = (uint32_t)(base + (int32_t)(r >> (15 - L)));
     br.drop(L);
     return (int)__builtin_amdgcn_readfirstlane((uint32_t)syms[idx]);
+}
+
+// Inclusive prefix sum / max over the 64 lanes (DPP row shifts, then row
+// broadcasts 15 and 31).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
 }
 
 __device__ __forceinline__ uint32_t coherent_load(const uint8_t* p) {
@@ -694,6 +719,126 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     const uint32_t m_mat = 0u - (uint32_t)((e & kFastMatch) != 0 && (ed & kFastDLong) == 0 && dist <= opos);
                     const uint32_t info = (lit & m_lit) | (mat & m_mat & ~m_lit);
                     GZP(7, 1);
+#if MSW_GZ_WPE
+                    // Lane-parallel emission.  The chain is found first, on the
+                    // scalar unit, from a per-lane "next token's lane" (255: this
+                    // lane's token is not simple): three scalar ops per token.
+                    // Then the window's output -- W bytes from opos -- is made by
+                    // lane b = output byte b: the token covering it (a prefix sum
+                    // of the chain tokens' output lengths, their lanes scattered
+                    // to their first byte and spread by a prefix max), then a
+                    // literal byte, a ring byte, a byte of the flushed output in
+                    // L2, or (a match reading this window's own output) the value
+                    // of an earlier lane, by pointer jumping; one ring write.
+                    // Windows of more than 64 output bytes take the serial walk.
+                    const uint32_t nbits = (info & 0x40000000u) ? (info & 63u) : (info & 15u);
+                    const uint32_t nx = (int32_t)info < 0 ? lane + nbits : 255u;
+                    uint64_t cmask = 0;  // bit L: lane L's token is on the chain
+                    k = 0;
+                    for (;;) {
+                        const uint32_t kn = (uint32_t)__builtin_amdgcn_readlane((int)nx, (int)k);
+                        if (kn == 255u) break;
+                        asm("s_bitset1_b64 %0, %1" : "+s"(cmask) : "s"(k));
+                        k = kn;
+                        if (k >= 64) break;
+                    }
+                    uint32_t on;
+                    asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(on) : "s"(cmask));
+                    const uint32_t m_match = 0u - ((info >> 30) & 1u);
+                    const uint32_t olen = (0u - on) & ((((info >> 6) & 511u) & m_match) | (((info >> 4) & 3u) & ~m_match));
+                    const uint32_t incl = wave_incl_sum(olen);
+                    const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                    if (W <= 64u) {
+                        if (W) {
+                            const uint32_t ost = incl - olen;  // the token's first output byte (window-relative)
+                            // the 64 dummy bytes as scratch; lanes read what other lanes
+                            // wrote, so a barrier (the block is this one wave) keeps the
+                            // compiler from forwarding a lane's own store to its load
+                            uint8_t* scr = ring + RING;
+                            scr[lane] = 0;
+                            if (on) scr[ost] = (uint8_t)(lane + 1u);
+                            __syncthreads();
+                            const uint32_t tl = wave_incl_max((uint32_t)scr[lane]) - 1u;  // lane of my byte's token
+                            const int ta = (int)(min(tl, 63u) << 2);
+                            const uint32_t ti = (uint32_t)__builtin_amdgcn_ds_bpermute(ta, (int)info);
+                            const uint32_t to = (uint32_t)__builtin_amdgcn_ds_bpermute(ta, (int)ost);
+                            const uint32_t off = lane - to;
+                            const bool lit = (ti & 0x40000000u) == 0;
+                            const uint32_t d = ((ti >> 15) & 0x7FFFu) + 1u;
+                            // overlapping copies repeat the token's last d bytes
+                            const float rd = __builtin_amdgcn_rcpf((float)d);
+                            int32_t r = (int32_t)off - (int32_t)((uint32_t)((float)off * rd)) * (int32_t)d;
+                            r += r < 0 ? (int32_t)d : 0;
+                            r -= r >= (int32_t)d ? (int32_t)d : 0;
+                            const int32_t src = (int32_t)(to + (uint32_t)r) - (int32_t)d;  // window-relative source
+                            const bool dep = !lit && src >= 0;
+                            const bool far = !lit && src < -(int32_t)RING;
+                            uint32_t val = lit ? (((ti >> 6) >> (8u * (off & 3u))) & 0xFFu)
+                                               : (uint32_t)ring[(opos + (uint32_t)src) & kRingMask];
+                            if (__builtin_amdgcn_ballot_w64(far && lane < W)) {
+                                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the flush stores have landed
+                                const uint64_t q = mem.ooff + (uint64_t)(far ? opos + (uint32_t)src : 0u);
+                                const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
+                                if (far) val = (w >> (8u * (uint32_t)(q & 3))) & 0xFFu;
+                            }
+                            // bytes made by an earlier lane of this window
+                            uint32_t ptr = dep ? (uint32_t)src : lane;
+                            uint32_t done = dep ? 0u : 1u;
+                            while (__builtin_amdgcn_ballot_w64(done == 0u && lane < W)) {
+                                const int pa = (int)(ptr << 2);
+                                const uint32_t tv = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)val);
+                                const uint32_t td = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)done);
+                                const uint32_t tp = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)ptr);
+                                if (!done) {
+                                    if (td) { val = tv; done = 1u; }
+                                    else ptr = tp;
+                                }
+                            }
+                            if (lane < W) ring[(opos + lane) & kRingMask] = (uint8_t)val;
+                            GZP(5, 1);
+                            opos += W;
+                            if (__builtin_expect(opos - flushed >= kChunk, 0)) {
+                                if (opos > isize) bad = GZ_E_OVERRUN;
+                                else do { flush_chunk(flushed); flushed += kChunk; } while (opos - flushed >= kChunk);
+                            }
+                        }
+                    } else {
+                        GZP(2, 1);
+                        // the walk: one exit (k past the window); a token the window
+                        // cannot take, or an overrun, ends it by pushing k out of range
+                        k = 0;
+                        uint32_t kstop = 0;
+                        do {
+                            const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k);
+                            if (s & 0x40000000u) {
+                                const uint32_t ln = (s >> 6) & 511u, ds = ((s >> 15) & 0x7FFFu) + 1u;
+                                GZP(5, 1);
+                                copy_match(ln, ds);
+                                opos += ln;
+                                k += s & 63u;
+                            } else if ((int32_t)s < 0) {
+                                GZP(2, 1);
+                                const uint32_t nlit = (s >> 4) & 3u;
+                                ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(s >> lit_shift6);
+                                opos += nlit;
+                                k += s & 15u;
+                            } else {
+                                kstop = k;  // not a simple token: the scalar step takes it
+                                k = 0x10000u;
+                            }
+                            if (__builtin_expect(opos - flushed >= kChunk, 0)) {
+                                if (opos > isize) {
+                                    bad = GZ_E_OVERRUN;
+                                    kstop = k;
+                                    k = 0x10000u;
+                                } else {
+                                    do { flush_chunk(flushed); flushed += kChunk; } while (opos - flushed >= kChunk);
+                                }
+                            }
+                        } while (k < 64);
+                        if (k == 0x10000u) k = kstop;
+                    }
+#else
                     // the walk: one exit (k past the window); a token the window
                     // cannot take, or an overrun, ends it by pushing k out of range
                     k = 0;
@@ -727,6 +872,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                         }
                     } while (k < 64);
                     if (k == 0x10000u) k = kstop;
+#endif
                     pb += k;
                     pw += pb >> 5;
                     pb &= 31u;
