@@ -365,27 +365,6 @@ __device__ __forceinline__ int decode_sym(Bits& br, uint32_t lim, int32_t bas, c
     return (int)__builtin_amdgcn_readfirstlane((uint32_t)syms[idx]);
 }
 
-// Inclusive prefix sum / max over the 64 lanes (DPP row shifts, then row
-// broadcasts 15 and 31).
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
-    return v;
-}
-
 __device__ __forceinline__ uint32_t coherent_load(const uint8_t* p) {
     return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -720,48 +699,38 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     const uint32_t info = (lit & m_lit) | (mat & m_mat & ~m_lit);
                     GZP(7, 1);
 #if MSW_GZ_WPE
-                    // Lane-parallel emission.  The chain is found first, on the
-                    // scalar unit, from a per-lane "next token's lane" (255: this
-                    // lane's token is not simple): three scalar ops per token.
-                    // Then the window's output -- W bytes from opos -- is made by
-                    // lane b = output byte b: the token covering it (a prefix sum
-                    // of the chain tokens' output lengths, their lanes scattered
-                    // to their first byte and spread by a prefix max), then a
-                    // literal byte, a ring byte, a byte of the flushed output in
-                    // L2, or (a match reading this window's own output) the value
-                    // of an earlier lane, by pointer jumping; one ring write.
-                    // Windows of more than 64 output bytes take the serial walk.
-                    const uint32_t nbits = (info & 0x40000000u) ? (info & 63u) : (info & 15u);
-                    const uint32_t nx = (int32_t)info < 0 ? lane + nbits : 255u;
-                    uint64_t cmask = 0;  // bit L: lane L's token is on the chain
+                    // Lane-parallel emission.  The chain is walked on the scalar
+                    // unit from a per-lane record "next token's lane (255: this
+                    // lane's token is not simple) | output length << 8"; at each
+                    // chain token every output lane b >= (bytes so far) takes the
+                    // token's record and first byte (a later token overwrites), so
+                    // after the walk lane b holds the token covering output byte
+                    // b.  Then lane b makes that byte -- a literal byte, a ring
+                    // byte, a byte of the flushed output in L2, or (a match
+                    // reading this window's own output) the value of an earlier
+                    // lane by pointer jumping -- and one ring write stores the
+                    // window's W bytes.  Windows of more than 64 output bytes take
+                    // the serial walk.
+                    const uint32_t m_match = 0u - ((info >> 30) & 1u);
+                    const uint32_t olen = (((info >> 6) & 511u) & m_match) | (((info >> 4) & 3u) & ~m_match);
+                    const uint32_t nbits = ((info & 63u) & m_match) | ((info & 15u) & ~m_match);
+                    const uint32_t nxo = ((int32_t)info < 0 ? lane + nbits : 255u) | (olen << 8);
+                    uint32_t W = 0, ti = 0, to = 0;
                     k = 0;
                     for (;;) {
-                        const uint32_t kn = (uint32_t)__builtin_amdgcn_readlane((int)nx, (int)k);
+                        const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)nxo, (int)k);
+                        const uint32_t kn = t & 255u;
                         if (kn == 255u) break;
-                        asm("s_bitset1_b64 %0, %1" : "+s"(cmask) : "s"(k));
+                        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k);
+                        const bool take = lane >= W;
+                        ti = take ? s0 : ti;
+                        to = take ? W : to;
+                        W += t >> 8;
                         k = kn;
                         if (k >= 64) break;
                     }
-                    uint32_t on;
-                    asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(on) : "s"(cmask));
-                    const uint32_t m_match = 0u - ((info >> 30) & 1u);
-                    const uint32_t olen = (0u - on) & ((((info >> 6) & 511u) & m_match) | (((info >> 4) & 3u) & ~m_match));
-                    const uint32_t incl = wave_incl_sum(olen);
-                    const uint32_t W = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                     if (W <= 64u) {
                         if (W) {
-                            const uint32_t ost = incl - olen;  // the token's first output byte (window-relative)
-                            // the 64 dummy bytes as scratch; lanes read what other lanes
-                            // wrote, so a barrier (the block is this one wave) keeps the
-                            // compiler from forwarding a lane's own store to its load
-                            uint8_t* scr = ring + RING;
-                            scr[lane] = 0;
-                            if (on) scr[ost] = (uint8_t)(lane + 1u);
-                            __syncthreads();
-                            const uint32_t tl = wave_incl_max((uint32_t)scr[lane]) - 1u;  // lane of my byte's token
-                            const int ta = (int)(min(tl, 63u) << 2);
-                            const uint32_t ti = (uint32_t)__builtin_amdgcn_ds_bpermute(ta, (int)info);
-                            const uint32_t to = (uint32_t)__builtin_amdgcn_ds_bpermute(ta, (int)ost);
                             const uint32_t off = lane - to;
                             const bool lit = (ti & 0x40000000u) == 0;
                             const uint32_t d = ((ti >> 15) & 0x7FFFu) + 1u;
@@ -781,18 +750,16 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                                 const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
                                 if (far) val = (w >> (8u * (uint32_t)(q & 3))) & 0xFFu;
                             }
-                            // bytes made by an earlier lane of this window
+                            // bytes made by an earlier lane of this window: follow
+                            // the pointers (a resolved lane points to itself)
                             uint32_t ptr = dep ? (uint32_t)src : lane;
-                            uint32_t done = dep ? 0u : 1u;
-                            while (__builtin_amdgcn_ballot_w64(done == 0u && lane < W)) {
+                            while (__builtin_amdgcn_ballot_w64(ptr != lane && lane < W)) {
                                 const int pa = (int)(ptr << 2);
                                 const uint32_t tv = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)val);
-                                const uint32_t td = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)done);
                                 const uint32_t tp = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)ptr);
-                                if (!done) {
-                                    if (td) { val = tv; done = 1u; }
-                                    else ptr = tp;
-                                }
+                                const bool settle = ptr != lane && tp == ptr;
+                                val = settle ? tv : val;
+                                ptr = settle ? lane : tp;
                             }
                             if (lane < W) ring[(opos + lane) & kRingMask] = (uint8_t)val;
                             GZP(5, 1);
