@@ -673,13 +673,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         const int per_gpu = std::max(1, atoi(env_or("MSW_GFASTQ_WORKERS_PER_GPU", "2").c_str()));
         const int nworkers = ngpu * per_gpu;
         gstats.assign((size_t)nworkers, msw_stats_t{});
-        // MSW_GFASTQ_STAGGER=1: a GPU's later workers start their first file
-        // once its first worker has launched its first scoring batch, so one
-        // worker's read + inflate + parse runs beside the other's scoring
-        // instead of both inflating, then both scoring
-        const bool stagger = env_or("MSW_GFASTQ_STAGGER", "0") != "0";
-        std::unique_ptr<std::atomic<int>[]> lead_scored(new std::atomic<int>[(size_t)ngpu]);
-        for (int g = 0; g < ngpu; ++g) lead_scored[g] = 0;
         for (int wi = 0; wi < nworkers; ++wi) {
             workers.emplace_back([&, wi]() {
                 const int gi = wi % ngpu;
@@ -817,9 +810,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     }
                 };
                 gate.arrive();
-                if (stagger && wi >= ngpu)
-                    while (!lead_scored[gi].load() && next_file.load() < todo.size())
-                        std::this_thread::sleep_for(std::chrono::microseconds(50));
                 // One loop over the batches of all of this worker's files: a
                 // file's last batches are settled after the next file's first
                 // batch is launched, so the next file's read, inflate and parse
@@ -861,7 +851,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         have = open_next(&fi);
                         continue;
                     }
-                    if (wi < ngpu) lead_scored[gi].store(1);
                     r.n = d.n;
                     r.first = d.first_read;
                     r.fi = fi;
