@@ -268,6 +268,10 @@ struct msw_ctx {
     int device = 0;
     int cu_count = 256;
     hipStream_t compute = nullptr, copy = nullptr, d2h = nullptr;
+    // multi-chunk calls alternate their chunks' kernels over compute and
+    // compute2, so chunk k+1's waves start under chunk k's tail (one stream
+    // would idle the CUs the tail leaves)
+    hipStream_t compute2 = nullptr;
     hipStream_t side = nullptr;  // long-pair launches beside packed ones (fork_side)
     // Staging slots, used round robin by successive chunks (and calls): with
     // three, the host stages chunk k+1 while k runs and k-1 drains, so the
@@ -666,7 +670,7 @@ int join_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
 bool use_wide_multi(size_t n_wide) { return use_multi(n_wide) && !getenv("MSW_NO_WIDE_MULTI"); }
 
 int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const std::vector<Bucket>& buckets,
-                   bool use_order, uint32_t read_stride, uint32_t win_stride) {
+                   bool use_order, uint32_t read_stride, uint32_t win_stride, hipStream_t cs) {
     const size_t n_short = short_buckets(buckets);
     SideFork side;
     if (n_short < buckets.size()) {  // long pairs: their own launch, beside any packed ones
@@ -685,10 +689,10 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.end_j = sch.coords ? s.d_ej : nullptr;
         p.read_stride = read_stride;
         p.win_stride = win_stride;
-        int rc = n_short ? fork_side(ctx, ctx->compute, side) : MSW_OK;
+        int rc = n_short ? fork_side(ctx, cs, side) : MSW_OK;
         if (!rc)
             rc = launch_long(sch, p, b.count, b.max_m, b.max_n, use_order && b.spread, ctx->cu_count,
-                             n_short ? ctx->side : ctx->compute);
+                             n_short ? ctx->side : cs);
         if (rc) return rc;
         if (n_short == 0) return MSW_OK;
     }
@@ -713,7 +717,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.out_slot_base = 0;
         msw::MultiTable t;
         fill_multi(buckets, 0, n_multi, sch, t);
-        HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
+        HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, cs));
         first_single = n_multi;
     }
     // the KR 17..24 buckets: one launch of the wide instance when there are
@@ -738,7 +742,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.out_slot_base = 0;
         msw::MultiTable t;
         fill_multi(buckets, n_multi, n_short, sch, t);
-        HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, ctx->compute));
+        HIP_TRY(msw::launch_sw_multi(p, t, sch.affine, sch.coords, cs));
         single_end = n_multi;
     }
     for (size_t bi = first_single; bi < single_end; ++bi) {
@@ -764,9 +768,9 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.pairs_blocks = plan.pairs_blocks;
         p.group_lanes = plan.group_lanes;
         p.groups = plan.groups;
-        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan.layout, ctx->compute));
+        HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan.layout, cs));
     }
-    if (side.ev) return join_side(ctx, ctx->compute, side);
+    if (side.ev) return join_side(ctx, cs, side);
     (void)n;
     return MSW_OK;
 }
@@ -920,7 +924,9 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
             (c == 0 && n > chunk) ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8) : chunk;
         cnt = std::min(this_chunk, n - first);
         // Slots alternate across calls too, so consecutive async calls overlap.
-        Slot& s = ctx->slots[ctx->slot_seq++ % msw_ctx::kSlots];
+        const uint64_t seq = ctx->slot_seq++;
+        Slot& s = ctx->slots[seq % msw_ctx::kSlots];
+        hipStream_t cs = (multi_chunk && (seq & 1)) ? ctx->compute2 : ctx->compute;
         if (tr.on) tr.submit += tr.lap();
         if ((rc = drain_slot(ctx, s))) return rc;  // the slot's previous chunk must be out before reuse
         if (tr.on) tr.wait += tr.lap();
@@ -972,7 +978,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         // H2D on the copy stream, kernels on the compute stream (a one-chunk
         // batch has nothing to overlap: everything goes on the compute stream,
         // saving the cross-stream event).
-        hipStream_t up = multi_chunk ? ctx->copy : ctx->compute;
+        hipStream_t up = multi_chunk ? ctx->copy : cs;
         HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
         if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
         // [pos | order | rlen | wlen]: skip the parts this chunk does not use
@@ -987,15 +993,15 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
                                             cnt, up));
         if (multi_chunk) {
             HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
-            HIP_TRY(hipStreamWaitEvent(ctx->compute, s.uploaded, 0));
+            HIP_TRY(hipStreamWaitEvent(cs, s.uploaded, 0));
         }
         if (uniform) {
             buckets.resize(1);
             buckets[0].begin = 0;
         }
-        HIP_TRY(hipEventRecord(s.k_start, ctx->compute));
-        if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws))) return rc;
-        HIP_TRY(hipEventRecord(s.k_end, ctx->compute));
+        HIP_TRY(hipEventRecord(s.k_start, cs));
+        if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws, cs))) return rc;
+        HIP_TRY(hipEventRecord(s.k_end, cs));
         {
             uint64_t cells = 0, bytes = 0;
             for (uint64_t i = 0; i < cnt; ++i) {
@@ -1007,9 +1013,9 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
             ctx->stats.cells += cells;
             ctx->stats.alg_bytes += bytes + cnt * (sch.coords ? 8u : 4u);
         }
-        hipStream_t down = ctx->compute;
+        hipStream_t down = cs;
         if (multi_chunk) {
-            HIP_TRY(hipEventRecord(s.computed, ctx->compute));
+            HIP_TRY(hipEventRecord(s.computed, cs));
             HIP_TRY(hipStreamWaitEvent(ctx->d2h, s.computed, 0));
             down = ctx->d2h;
         }
@@ -1059,6 +1065,7 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
         const std::string msg = g_last_error;
         (void)hipStreamSynchronize(ctx->copy);
         (void)hipStreamSynchronize(ctx->compute);
+        (void)hipStreamSynchronize(ctx->compute2);
         (void)hipStreamSynchronize(ctx->d2h);
         (void)hipStreamSynchronize(ctx->side);
         for (Slot& s : ctx->slots)
@@ -1152,6 +1159,7 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
     if (e == hipSuccess && hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
@@ -1167,6 +1175,7 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->compute) (void)hipStreamSynchronize(ctx->compute);
+    if (ctx->compute2) (void)hipStreamSynchronize(ctx->compute2);
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
     if (ctx->d2h) (void)hipStreamSynchronize(ctx->d2h);
     if (ctx->side) (void)hipStreamSynchronize(ctx->side);
@@ -1192,6 +1201,7 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     for (hipEvent_t e : ctx->free_events) (void)hipEventDestroy(e);
     for (auto& kv : ctx->fences) (void)hipEventDestroy(kv.second);
     if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
+    if (ctx->compute2) (void)hipStreamDestroy(ctx->compute2);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -1735,6 +1745,7 @@ int msw_synchronize(msw_ctx* ctx) {
     int rc = set_device(ctx);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->compute));
+    HIP_TRY(hipStreamSynchronize(ctx->compute2));
     HIP_TRY(hipStreamSynchronize(ctx->copy));
     HIP_TRY(hipStreamSynchronize(ctx->d2h));
     HIP_TRY(hipGetLastError());
