@@ -616,7 +616,7 @@ def leg_pairs(job, ctx, cfg, args):
             "gen_seconds": round(gen_s, 1)}
 
 
-def leg_h2h(job, ctx, batch, scoring, dev_res, chunk=65536):
+def leg_h2h(job, ctx, batch, scoring, dev_res, chunk=32768):
     """configs_extra.config3.host_to_host -- BASELINE config 3 as stated
     ("async FASTQ chunk staging"): the rank's pairs start in pinned host
     memory (msw_host_alloc, aligner.rs:466-475 USE_PINNED_MEMORY) and go
@@ -628,7 +628,11 @@ def leg_h2h(job, ctx, batch, scoring, dev_res, chunk=65536):
     shard's windows back to back, so the cut windows are exactly the batch's)
     and the reads + windows themselves (msw_align_batch).  Setup (genome
     upload, pinned fills) is outside the timed calls; each call is bracketed
-    by the job fence; best of 3; results must equal the HBM-resident run."""
+    by the job fence; best of 3; results must equal the HBM-resident run.
+    Chunks of 32 K pairs: with the chunks' kernels alternating over two
+    compute streams, 16 K / 32 K / 64 K / 128 K pairs run 5.18-5.21 /
+    5.16-5.18 / 4.99-5.03 / 4.83-4.86 TCUPS (tools/h2h_sweep.py,
+    profiles/r03/h2h/chunk_sweep_two_streams.jsonl)."""
     from mini_parallel_amd.aligner import pinned_empty
 
     def pinned(a):
