@@ -10,21 +10,24 @@
 // members inflates with thousands of waves at once and only compressed bytes
 // cross PCIe.
 //
-// Mapping.  Huffman decoding is a serial chain per member, so a wave owns a
-// member and runs the chain on wave-uniform values (SGPRs; the compiler sees
-// them as uniform); the 64 lanes are used where the format is parallel:
-//  * canonical decode without lookup tables: lane L (1..15) holds the
-//    left-justified end of the codes of length <= L; one compare + ballot
-//    finds the code length of the next 15 stream bits, v_readlane fetches the
-//    length's base, and ONE LDS read maps the code to its symbol (the
-//    sorted-symbol array, <= 288 u16), so a dynamic block's tables cost
-//    ~650 B of LDS and a few hundred instructions to build;
-//  * the last 4 KiB of output live in an LDS ring: literals are single-lane
-//    byte writes, a match copies up to 64 bytes per instruction from the ring
-//    (overlapping copies index the source modulo the distance), and every
-//    completed 256-byte chunk is flushed to HBM with one coalesced store per
-//    lane; matches reaching further back than the ring read the flushed
-//    output from L2 (agent-scope loads after the flush stores have drained);
+// Mapping.  A wave owns a member.  Block headers and table builds run on
+// wave-uniform values with the 64 lanes where the format is parallel
+// (canonical code tables by ballots; 9-bit literal/length and 7-bit distance
+// lookup tables in LDS).  The Huffman data is decoded by speculative windows:
+//  * the only serial fact is where the next token starts, so lane L decodes
+//    the token that would start at bit P + L (both table lookups, length and
+//    distance with their extra bits) into a record; the scalar unit walks the
+//    chain of records (token at lane k, next at k + its bits), and at each
+//    chain token the output lanes from its first byte on take its record;
+//  * lane b then makes output byte b of the window -- a literal byte, a byte
+//    of the 2 KiB output ring in LDS (j mod dist back for overlapping
+//    copies), a byte of the flushed output in L2, or an earlier lane's value
+//    by pointer jumping when a match reads this window's own output -- and
+//    one masked write stores the window's bytes in the ring; every completed
+//    256-byte chunk is flushed to HBM with one coalesced store per lane;
+//  * windows producing more than 64 bytes take a serial walk of the same
+//    records, and tokens no window resolves (long codes, end of block,
+//    invalid codes, the member's last bits) a one-token scalar step;
 //  * the CRC-32 check is a second kernel: a wave reads the member's output
 //    in coalesced 256-byte chunks, lane l folds dword l of every chunk into
 //    its own state with a table-driven 256-byte advance, and the 64 lane
@@ -52,14 +55,6 @@ constexpr int kDefaultRingKb = 2;  // best measured throughput (tools/inflate_be
 #define GZP(i, v) (pc[i] += (v))
 #else
 #define GZP(i, v) ((void)0)
-#endif
-// MSW_GZ_SPEC=0 builds the one-token-at-a-time Huffman loop (A/B variant)
-#ifndef MSW_GZ_SPEC
-#define MSW_GZ_SPEC 1
-#endif
-// MSW_GZ_WPE=1: a window's output made lane-parallel (=0: the serial walk)
-#ifndef MSW_GZ_WPE
-#define MSW_GZ_WPE 1
 #endif
 
 constexpr uint32_t kChunk = 256;  // flush unit: 64 lanes x 4 bytes
@@ -577,7 +572,6 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 return L | kFastMatch | ((L + x) << 8) | (x << 16) | (b << 23);
             };
             if (!br.refill()) { err = GZ_E_TRUNC; break; }
-#if MSW_GZ_SPEC
             // Speculative window decode.  The serial part of inflate is only
             // "where does the next token start"; everything else about a token
             // (table lookups, length and distance with their extra bits) is a
@@ -698,7 +692,6 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     const uint32_t m_mat = 0u - (uint32_t)((e & kFastMatch) != 0 && (ed & kFastDLong) == 0 && dist <= opos);
                     const uint32_t info = (lit & m_lit) | (mat & m_mat & ~m_lit);
                     GZP(7, 1);
-#if MSW_GZ_WPE
                     // Lane-parallel emission.  The chain is walked on the scalar
                     // unit from a per-lane record "next token's lane (255: this
                     // lane's token is not simple) | output length << 8"; at each
@@ -805,41 +798,6 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                         } while (k < 64);
                         if (k == 0x10000u) k = kstop;
                     }
-#else
-                    // the walk: one exit (k past the window); a token the window
-                    // cannot take, or an overrun, ends it by pushing k out of range
-                    k = 0;
-                    uint32_t kstop = 0;
-                    do {
-                        const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k);
-                        if (s & 0x40000000u) {
-                            const uint32_t ln = (s >> 6) & 511u, ds = ((s >> 15) & 0x7FFFu) + 1u;
-                            GZP(5, 1);
-                            copy_match(ln, ds);
-                            opos += ln;
-                            k += s & 63u;
-                        } else if ((int32_t)s < 0) {
-                            GZP(2, 1);
-                            const uint32_t nlit = (s >> 4) & 3u;
-                            ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(s >> lit_shift6);
-                            opos += nlit;
-                            k += s & 15u;
-                        } else {
-                            kstop = k;  // not a simple token: the scalar step takes it
-                            k = 0x10000u;
-                        }
-                        if (__builtin_expect(opos - flushed >= kChunk, 0)) {
-                            if (opos > isize) {
-                                bad = GZ_E_OVERRUN;
-                                kstop = k;
-                                k = 0x10000u;
-                            } else {
-                                do { flush_chunk(flushed); flushed += kChunk; } while (opos - flushed >= kChunk);
-                            }
-                        }
-                    } while (k < 64);
-                    if (k == 0x10000u) k = kstop;
-#endif
                     pb += k;
                     pw += pb >> 5;
                     pb &= 31u;
@@ -922,136 +880,6 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 err = bad;
                 break;
             }
-#else
-            uint32_t ev = lookup();
-            // One exit: every failure lands in `bad` (the literal run masks its
-            // next entry to "not a literal", the match path checks once before
-            // it copies), which keeps the loop free of the exit-selector blocks
-            // a many-exit loop compiles to.  Every token starts with >= 32 bits
-            // in the buffer (a refill follows every drop of a token's last bits).
-            uint32_t bad = 0;
-            for (;;) {
-                uint32_t e = __builtin_amdgcn_readfirstlane(ev);
-                if (__builtin_expect((e & kFastLong) != 0, 0)) e = slow_ll();
-                if (e & 0x30u) {
-                    // Literal runs: a tight inner loop while the lookups yield
-                    // literals (1..3 per entry: lane k writes the k-th).
-                    uint32_t ok = ~0u;
-                    do {
-                        const uint32_t nlit = (e >> 4) & 3u;
-                        GZP(2, 1);
-                        GZP(3, nlit);
-                        br.drop(e & 15u);
-                        if (br.bcnt < 32) br.refill_fast();
-                        ev = lookup();
-                        ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(e >> lit_shift);
-                        opos += nlit;
-                        if (opos - flushed >= kChunk && !flush_to()) { bad = GZ_E_OVERRUN; ok = 0; }
-                        e = __builtin_amdgcn_readfirstlane(ev) & ok;
-                    } while (e & 0x30u);
-                    if (bad) break;
-                    continue;  // the next entry is re-dispatched at the top
-                }
-                GZP(4, 1);
-                if (!(e & kFastMatch)) {  // end of block, or no code of this set
-                    if (e & kFastBadE) bad = GZ_E_SYMBOL;
-                    else br.drop(e & 15u);
-                    break;
-                }
-                // a length code: the entry is the s_bfe control of its extra
-                // bits; base + extra, code + extra bits dropped
-                // (the first failure of a token is the one reported: bad = bad ? bad : code)
-                const uint32_t len = (e >> 23) + sbfe((uint32_t)br.bb, e);
-                br.drop((e >> 8) & 63u);
-                if (br.bcnt < 32) br.refill_fast();
-                // distance, the same way (base from the parallel table)
-                const uint32_t di = (uint32_t)br.bb & ((1u << kFastDBits) - 1u);
-                uint32_t ed = __builtin_amdgcn_readfirstlane(S.fast_d[di]);
-                uint32_t dbase = __builtin_amdgcn_readfirstlane(S.fast_dbase[di]);
-                if (__builtin_expect((ed & kFastDLong) != 0, 0)) {
-                    // longer than the table: canonical decode into an entry
-                    const uint32_t r = __builtin_bitreverse32((uint32_t)br.bb) >> 17;
-                    const uint64_t m = __ballot(r < lim_d);
-                    uint32_t L = 0, d = 31;
-                    if (m) {
-                        L = (uint32_t)__builtin_ctzll(m);
-                        const int32_t base = __builtin_amdgcn_readlane(bas_d, (int)L);
-                        d = __builtin_amdgcn_readfirstlane((uint32_t)S.sym_d[(uint32_t)(base + (int32_t)(r >> (15 - L)))]);
-                    }
-                    ed = 0;
-                    dbase = 0xFFFFFFFFu;  // no code: fails the distance test below, reported as SYMBOL
-                    if (d > 29) {
-                        bad = GZ_E_SYMBOL;  // bad == 0 on entry
-                    } else {
-                        uint32_t x;
-                        dbase = dist_base(d, x);
-                        ed = L | ((L + x) << 8) | (x << 16);
-                    }
-                }
-                const uint32_t dist = dbase + sbfe((uint32_t)br.bb, ed);  // ed == 0 for no code: dbase
-                br.drop((ed >> 8) & 31u);
-                if (br.bcnt < 32) br.refill_fast();
-                if (__builtin_expect(dist > opos, 0)) {  // too far back, or no distance code
-                    bad = bad ? bad : (uint32_t)GZ_E_DIST;
-                    break;
-                }
-                ev = lookup();  // the next token's entry, in flight during the copy
-                GZP(5, 1);
-#if MSW_GZ_PROFILE
-                const uint64_t t_copy = __builtin_amdgcn_s_memtime();
-#endif
-                if (dist + len <= kRing) {
-                    // ring -> ring, 64 bytes per instruction pair; byte j copies
-                    // source byte j mod dist (overlapping copies repeat the last
-                    // `dist` bytes; j mod dist = j when dist >= len).  Inactive
-                    // lanes move their dummy byte.
-                    const float rd = __builtin_amdgcn_rcpf((float)dist);
-                    uint32_t j0 = 0;
-                    do {
-                        const uint32_t j = j0 + lane;
-                        int32_t r = (int32_t)j - (int32_t)((uint32_t)((float)j * rd)) * (int32_t)dist;
-                        r += r < 0 ? (int32_t)dist : 0;
-                        r -= r >= (int32_t)dist ? (int32_t)dist : 0;
-                        // lane select by arithmetic, not a select the compiler
-                        // may turn into an exec-mask branch around the modulo
-                        const uint32_t on = 0u - (uint32_t)(j < len);
-                        const uint32_t src = ((opos - dist + (uint32_t)r) & kRingMask) & on;
-                        const uint32_t dsti = ((opos + j) & kRingMask) & on;
-                        const uint8_t v = ring[src | (dummy & ~on)];
-                        ring[dsti | (dummy & ~on)] = v;
-                        j0 += 64;
-                    } while (j0 < len);
-                } else {
-                    // further back than the ring: the flushed output in L2 (the
-                    // source ends well before `flushed`)
-                    GZP(6, 1);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flush stores have landed
-                    // lane j fetches byte j (the dword holding it; a wave's 64
-                    // bytes are a few coalesced lines) -- no per-lane loops
-                    uint32_t j0 = 0;
-                    do {
-                        const uint32_t j = j0 + lane;
-                        const bool on = j < len;
-                        const uint64_t q = mem.ooff + (uint64_t)(opos - dist + (on ? j : 0u));
-                        const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
-                        ring[on ? ((opos + j) & kRingMask) : dummy] = (uint8_t)(w >> (8u * (uint32_t)(q & 3)));
-                        j0 += 64;
-                    } while (j0 < len);
-                }
-#if MSW_GZ_PROFILE
-                GZP(10, (uint32_t)(__builtin_amdgcn_s_memtime() - t_copy));
-#endif
-                opos += len;
-                if (opos - flushed >= kChunk && !flush_to()) {
-                    bad = GZ_E_OVERRUN;
-                    break;
-                }
-            }
-            if (bad) {
-                err = bad;
-                break;
-            }
-#endif
         }
         // a decode that ran into the bytes after the member (its last refills
         // merge them unchecked) failed because the member is truncated
