@@ -225,10 +225,11 @@ struct Inflater {
             double sum[12] = {0};
             for (uint32_t m = 0; m < n; ++m)
                 for (int i = 0; i < 12; ++i) sum[i] += h[(size_t)m * 16 + i];
-            const char* names[12] = {"cycles", "hdr_cycles", "lit_iters", "lit_bytes", "sym_entries", "matches",
-                                     "far_matches", "refills", "flushes", "blocks", "copy_cycles", "-"};
+            const char* names[12] = {"cycles", "hdr_cycles", "walk_lits", "win_decode_cycles", "scalar_steps",
+                                     "windows_emitted", "far_copies", "windows", "near_cycles", "blocks",
+                                     "far_cycles", "win_emit_cycles"};
             fprintf(stderr, "[gzprof] per member:");
-            for (int i = 0; i < 11; ++i) fprintf(stderr, " %s=%.0f", names[i], sum[i] / n);
+            for (int i = 0; i < 12; ++i) fprintf(stderr, " %s=%.0f", names[i], sum[i] / n);
             fprintf(stderr, "\n");
             (void)hipFree(d_prof);
         }

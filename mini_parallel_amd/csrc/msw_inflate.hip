@@ -660,6 +660,9 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 uint32_t k = 64;
                 const bool room = pw < pw_last || (pw == pw_last && ew >= 4u && eb + 16u >= pb);
                 if (room) {  // every candidate token ends inside the member
+#if MSW_GZ_PROFILE
+                    const uint64_t t_w = __builtin_amdgcn_s_memtime();
+#endif
                     if (pw - br.wbase > 59u) {
                         br.wbase = pw;
                         br.cur = br.src[pw + lane];
@@ -692,6 +695,11 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     const uint32_t m_mat = 0u - (uint32_t)((e & kFastMatch) != 0 && (ed & kFastDLong) == 0 && dist <= opos);
                     const uint32_t info = (lit & m_lit) | (mat & m_mat & ~m_lit);
                     GZP(7, 1);
+#if MSW_GZ_PROFILE
+                    (void)__builtin_amdgcn_readfirstlane(info);  // the decode has landed
+                    const uint64_t t_k = __builtin_amdgcn_s_memtime();
+                    GZP(3, (uint32_t)(t_k - t_w));
+#endif
                     // Lane-parallel emission.  The chain is walked on the scalar
                     // unit from a per-lane record "next token's lane (255: this
                     // lane's token is not simple) | output length << 8"; at each
@@ -707,21 +715,24 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     const uint32_t m_match = 0u - ((info >> 30) & 1u);
                     const uint32_t olen = (((info >> 6) & 511u) & m_match) | (((info >> 4) & 3u) & ~m_match);
                     const uint32_t nbits = ((info & 63u) & m_match) | ((info & 15u) & ~m_match);
-                    const uint32_t nxo = ((int32_t)info < 0 ? lane + nbits : 255u) | (olen << 8);
+                    // (a lane whose token is not simple: next lane 255, length 0)
+                    const uint32_t nxo = (int32_t)info < 0 ? (lane + nbits) | (olen << 8) : 255u;
                     uint32_t W = 0, ti = 0, to = 0;
+                    // one exit: k leaves the window (>= 64) or hits a token that
+                    // is not simple (255; the token at kp, which added nothing)
+                    uint32_t kp = 0;
                     k = 0;
-                    for (;;) {
+                    do {
                         const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)nxo, (int)k);
-                        const uint32_t kn = t & 255u;
-                        if (kn == 255u) break;
                         const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k);
                         const bool take = lane >= W;
                         ti = take ? s0 : ti;
                         to = take ? W : to;
                         W += t >> 8;
-                        k = kn;
-                        if (k >= 64) break;
-                    }
+                        kp = k;
+                        k = t & 255u;
+                    } while (k < 64);
+                    if (k == 255u) k = kp;
                     if (W <= 64u) {
                         if (W) {
                             const uint32_t off = lane - to;
@@ -798,6 +809,9 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                         } while (k < 64);
                         if (k == 0x10000u) k = kstop;
                     }
+#if MSW_GZ_PROFILE
+                    GZP(11, (uint32_t)(__builtin_amdgcn_s_memtime() - t_k));
+#endif
                     pb += k;
                     pw += pb >> 5;
                     pb &= 31u;
