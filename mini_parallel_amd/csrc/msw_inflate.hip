@@ -1062,6 +1062,7 @@ hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint
 #define GZ_LAUNCH(R) hipLaunchKernelGGL(gz_inflate_kernel<R>, dim3(grid), dim3(64), lds_pad, stream, cdata, members, n, \
                                          out, status, any_error, prof)
     switch (ring_kb) {
+        case 1: GZ_LAUNCH(1024); break;
         case 2: GZ_LAUNCH(2048); break;
         case 4: GZ_LAUNCH(4096); break;
         case 16: GZ_LAUNCH(16384); break;
