@@ -84,8 +84,11 @@ I32_OPS_PER_CELL = {"linear": 6, "linear_coords": 8, "affine": 11, "affine_coord
 # SIMD, config 2: 1000 waves on 1024 SIMDs) at best every 4.75 cycles.
 PACKED_ISSUE_CYCLES, LONE_WAVE_ISSUE_CYCLES = 4.1, 4.75
 
-# config-4 leg: 8 lanes x R1/R2 BGZF lane files (aligner.rs:198-204 naming)
-C4_LANES, C4_READS_PER_LANE, C4_READS_PER_FILE = 8, 2, 2_000_000
+# config-4 leg: 8 lanes x R1/R2 BGZF lane files (aligner.rs:198-204 naming) of
+# 25 M reads = 400 M reads (BASELINE config 4: "8 lanes x ~50 M reads"), each
+# file 25 segments of 1 M reads from a pool of 32 distinct pre-scored segments
+C4_LANES, C4_READS_PER_LANE, C4_READS_PER_FILE = 8, 2, 25_000_000
+C4_SEGMENT_READS, C4_POOL = 1_000_000, 32
 C4_GENOME, C4_WINDOW, C4_LEVEL, C4_QUAL, C4_SEED = 64 << 20, 300, 6, "binned", 1004
 
 
@@ -131,8 +134,13 @@ def parse(argv=None):
     ap.add_argument("--c5-pairs", type=int, default=0, help="config-5 leg: pairs per GPU (default 100k)")
     ap.add_argument("--c4-reads-per-file", type=int, default=C4_READS_PER_FILE,
                     help="config-4 leg: reads per lane file (8 lanes x 2 files)")
+    ap.add_argument("--c4-segment-reads", type=int, default=C4_SEGMENT_READS,
+                    help="config-4 leg: reads per pooled segment (lane files are made of segments)")
+    ap.add_argument("--c4-pool", type=int, default=C4_POOL, help="config-4 leg: distinct segments in the pool")
+    ap.add_argument("--c3-fastq-reads", type=int, default=1_000_000,
+                    help="config-3 FASTQ leg: reads over its 16 lane files (0 = skip the leg)")
     ap.add_argument("--c4-dir", default="/tmp/msw_bench_c4",
-                    help="config-4 leg: where the lane files are generated (reused across runs)")
+                    help="configs 3 / 4 FASTQ legs: where the lane files are generated (reused across runs)")
     ap.add_argument("--no-h2h", action="store_true", help="config-3 leg: skip the host-to-host rate")
     ap.add_argument("--cpu-standin", action="store_true",
                     help="TEST ONLY (tests/test_bench_launcher.py): gloo ranks on the CPU with a "
@@ -234,7 +242,7 @@ def _oracle_kw(scoring):
                 gap_extend=scoring.gap_extend, affine=scoring.affine)
 
 
-def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j):
+def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j, seconds=None):
     """The CPU baseline, timed on this host: the inter-sequence SIMD
     restatement of the oracle (oracle/sw_simd.c, AVX-512BW 32 x int16 lanes /
     AVX2 16, bit-exact with the scalar oracle by tests/test_oracle.py) over a
@@ -244,6 +252,7 @@ def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j):
     whole sample and vs the scalar oracle on its smaller sample."""
     from oracle import oracle_lib
     oracle_lib.build()
+    budget = args.cpu_seconds if seconds is None else seconds
     aff, quota, usable = host_cpus()
     threads = args.cpu_threads or usable
     kw = _oracle_kw(scoring)
@@ -261,8 +270,8 @@ def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j):
     ts = time.perf_counter()
     simd(n0, threads)
     rate = n0 / max(time.perf_counter() - ts, 1e-6)
-    ns = int(min(batch.n_pairs, max(n0, rate * args.cpu_seconds)))
-    passes = max(1, int(rate * args.cpu_seconds / ns))
+    ns = int(min(batch.n_pairs, max(n0, rate * budget)))
+    passes = max(1, int(rate * budget / ns))
     ts = time.perf_counter()
     for _ in range(passes):
         cs, ci, cj, isa = simd(ns, threads)
@@ -281,7 +290,7 @@ def cpu_baseline(args, batch, scoring, gpu_scores, gpu_i, gpu_j):
         simd(ns, aff)
         all_aff = {"threads": aff, "gcups": round(cells_of(ns) / (time.perf_counter() - ts) / 1e9, 3)}
     # scalar oracle, one core, ~1/5 of the budget
-    n1 = max(1, min(ns, int(args.cpu_seconds * 0.2 * 2e8 / max(cells_of(1), 1))))
+    n1 = max(1, min(ns, int(budget * 0.2 * 2e8 / max(cells_of(1), 1))))
     ts = time.perf_counter()
     ss, si, sj = oracle_lib.sw_batch(batch.reads[:n1], batch.read_len[:n1], batch.wins[:n1],
                                      batch.win_len[:n1], threads=1, **kw)
@@ -514,8 +523,9 @@ class Job:
             torch.cuda.synchronize(self.dev)
 
     def fence(self):
+        from mini_parallel_amd import dist as mdist
         self.sync()
-        if self.world > 1:
+        if mdist.active():
             import torch.distributed as dist
             dist.barrier()
         self.sync()
@@ -599,6 +609,16 @@ def leg_pairs(job, ctx, cfg, args):
     else:
         want = standin_scores(config_shard(cfg, 0, n_total))
         par = {"standin": True, "gather_in_order": bool(np.array_equal(g[0], want)), "pairs": int(g[0].size)}
+    cpu = None
+    if job.gpu and args.cpu_seconds > 0:
+        # the CPU baseline of this leg's own pairs (rank 0's shard; BASELINE.md's
+        # plan), which also checks that shard's sample bit for bit
+        n0 = batch.n_pairs
+        cpu, cpar = cpu_baseline(args, batch, scoring, g[0][:n0], g[1][:n0] if len(g) > 1 else None,
+                                 g[2][:n0] if len(g) > 2 else None, seconds=max(1.0, args.cpu_seconds / 2))
+        par["rank0_cpu_sample"] = cpar
+        par["bit_exact"] = bool(par["bit_exact"] and cpar["bit_exact"])
+        par["mismatches"] += cpar["mismatches"]
     kernel_gcups = batch.cells / kern / 1e9
     alg = alg_bytes_of(batch, scoring)
     return {"workload": f"config{cfg}: {per_gpu} pairs/GPU of one global {n_total}-pair batch, reads "
@@ -612,7 +632,7 @@ def leg_pairs(job, ctx, cfg, args):
             "valu": valu_block(kind, kernel_gcups),
             "roofline_hbm": {"achieved": round(alg / kern / 1e9, 2), "frac": round(alg / kern / 1e9 / HBM_PEAK_GBPS, 5),
                              "alg_bytes_per_launch": alg},
-            "parity": par, "gathered_pairs": int(g[0].size), "host_to_host": h2h,
+            "parity": par, "gathered_pairs": int(g[0].size), "host_to_host": h2h, "cpu_baseline": cpu,
             "gen_seconds": round(gen_s, 1)}
 
 
@@ -679,40 +699,225 @@ def leg_h2h(job, ctx, batch, scoring, dev_res, chunk=32768):
 
 
 # ---------------------------------------------------------------------------
-# config-4 leg: the --full-wgs stream over BGZF lane files
+# FASTQ-backed legs: lane files on disk -> the product's --full-wgs driver
+# (rustseq_mini) as a child process per rank.  Datasets are written once,
+# before any rank touches a GPU, and reused while their DONE.json matches.
 # ---------------------------------------------------------------------------
-def c4_layout(args):
-    R = args.c4_reads_per_file
-    d = os.path.join(args.c4_dir, f"l{C4_LANES}x{C4_READS_PER_LANE}_r{R}_g{C4_GENOME}_z{C4_LEVEL}{C4_QUAL}_s{C4_SEED}")
-    files = [os.path.join(d, "SYN_L%03d_R%d_001.fastq.gz" % (ln, r))
-             for ln in range(1, C4_LANES + 1) for r in range(1, C4_READS_PER_LANE + 1)]
-    return d, files
+_POOL_GENOME = None  # set before forking the generator pools (shared copy-on-write)
 
 
-def ensure_c4_dataset(args) -> dict:
-    """Write the config-4 lane set once (before any rank touches a GPU;
-    reused while its DONE.json matches the files on disk)."""
-    from mini_parallel_amd.synthetic import write_wgs_dataset
-    d, files = c4_layout(args)
-    marker = os.path.join(d, "DONE.json")
+def _lane_names(lanes, rpl):
+    return ["SYN_L%03d_R%d_001.fastq.gz" % (ln, r) for ln in range(1, lanes + 1) for r in range(1, rpl + 1)]
+
+
+def _write_reference(path, g, seed):
+    with open(path, "w") as f:
+        f.write(">synthetic seed=%d\n" % seed)
+        s = g.tobytes().decode()
+        f.write("\n".join(s[k:k + 80] for k in range(0, len(s), 80)) + "\n")
+
+
+def _marker_ok(d, names):
     try:
-        with open(marker) as f:
+        with open(os.path.join(d, "DONE.json")) as f:
             m = json.load(f)
-        if all(os.path.getsize(p) == m["sizes"][os.path.basename(p)] for p in files):
+        if all(os.path.getsize(os.path.join(d, n)) == m["sizes"][n] for n in names):
             return m
     except (OSError, ValueError, KeyError):
         pass
-    import shutil
-    shutil.rmtree(d, ignore_errors=True)
-    t0 = time.perf_counter()
-    write_wgs_dataset(d, sample="SYN", lanes=C4_LANES, reads_per_lane=C4_READS_PER_LANE,
-                      reads_per_file=args.c4_reads_per_file, genome_bases=C4_GENOME, keep_batches=False,
-                      workers=host_cpus()[2], bgzf=True, qual=C4_QUAL, compresslevel=C4_LEVEL, seed=C4_SEED)
-    m = {"sizes": {os.path.basename(p): os.path.getsize(p) for p in files},
-         "gen_seconds": round(time.perf_counter() - t0, 1)}
-    with open(marker + ".tmp", "w") as f:
+    return None
+
+
+def _write_marker(d, m):
+    p = os.path.join(d, "DONE.json")
+    with open(p + ".tmp", "w") as f:
         json.dump(m, f)
-    os.replace(marker + ".tmp", marker)
+    os.replace(p + ".tmp", p)
+
+
+def _run_pool(fn, jobs, workers, tag):
+    """Run generator jobs on a fork pool, printing progress every 20 s (a
+    silent minute would look like a hang to the GPU box's watchdog)."""
+    from multiprocessing import get_context
+    t0 = time.perf_counter()
+    with get_context("fork").Pool(max(1, min(workers, len(jobs)))) as pool:
+        res = pool.map_async(fn, jobs, chunksize=1)
+        while not res.ready():
+            res.wait(20)
+            print(f"[bench] {tag}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+        return res.get(), time.perf_counter() - t0
+
+
+def _c4_segment_job(job):
+    """One pooled config-4 segment: `n` reads of 150 bp (their own seeded
+    run, synthetic._lane_reads), FASTQ text with binned qualities, BGZF at
+    zlib level 6 as whole members without the EOF block (segments
+    concatenate into lane files), then the oracle's score of every read
+    against its genome window (one thread; the i64 sum is what a lane file
+    made of this segment adds)."""
+    from mini_parallel_amd.synthetic import _lane_reads, _lane_records, _with_windows, bgzf_compress
+    from oracle import oracle_lib
+    idx, n, path = job
+    g = _POOL_GENOME
+    b, pos, rng = _lane_reads(g, idx, n, 150, 2.0, C4_SEED, segment=1)
+    data = bgzf_compress(_lane_records(b, pos, rng, b"SYN", idx // 2 + 1, C4_QUAL), C4_LEVEL, eof_block=False)
+    with open(path, "wb") as f:
+        f.write(data)
+    w = _with_windows(g, b, pos)
+    t0 = time.perf_counter()
+    s, _, _, _ = oracle_lib.sw_batch_simd(w.reads, w.read_len, w.wins, w.win_len, threads=1, coords=False)
+    dt = time.perf_counter() - t0
+    return {"segment": idx, "reads": int(n), "bases": int(w.read_len.astype(np.int64).sum()),
+            "score": int(s.astype(np.int64).sum()), "cells": int(w.cells), "oracle_s": dt, "bytes": len(data)}
+
+
+def c4_layout(args):
+    """Directory, lane file paths and segment plan of the config-4 dataset:
+    16 lane files (8 lanes x R1/R2) of R reads each, lane file f made of
+    segments plan[f] of a pool of P distinct S-read segments."""
+    R, S, P = args.c4_reads_per_file, args.c4_segment_reads, args.c4_pool
+    if S <= 0 or R % S:
+        raise SystemExit(f"bench.py: --c4-reads-per-file {R} must be a multiple of --c4-segment-reads {S}")
+    d = os.path.join(args.c4_dir, f"l{C4_LANES}x{C4_READS_PER_LANE}_r{R}_seg{S}x{P}_g{C4_GENOME}_z{C4_LEVEL}"
+                                  f"{C4_QUAL}_s{C4_SEED}")
+    names = _lane_names(C4_LANES, C4_READS_PER_LANE)
+    nseg = R // S
+    plan = [[(f * nseg + s) % P for s in range(nseg)] for f in range(len(names))]
+    return d, [os.path.join(d, n) for n in names], plan
+
+
+def _copy_into(dst, srcs, tail):
+    """dst = the concatenation of the files srcs, then the bytes tail
+    (copy_file_range: in-kernel copies, reflinks where the file system has them)."""
+    with open(dst, "wb") as fo:
+        for s in srcs:
+            with open(s, "rb") as fi:
+                left = os.fstat(fi.fileno()).st_size
+                off = 0
+                while left > 0:
+                    k = os.copy_file_range(fi.fileno(), fo.fileno(), min(left, 1 << 30), off)
+                    if k <= 0:
+                        raise OSError(f"copy_file_range stalled copying {s}")
+                    off += k
+                    left -= k
+        fo.write(tail)
+        return fo.tell()
+
+
+def ensure_c4_dataset(args) -> dict:
+    """BASELINE config 4 at its stated size: 8 lanes x R1/R2 BGZF lane files
+    of 25 M 150 bp reads (400 M reads; aligner.rs:198-204 naming, 51,858,562
+    reads per file at aligner.rs:214).  A pool of P distinct 1 M-read
+    segments is generated and scored by the oracle once; each lane file is
+    the concatenation of 25 pooled segments (BGZF members concatenate into a
+    valid multi-member gzip), so its expected (score i64, reads, bases) is
+    the sum over its segments.  Segments repeat across and within files --
+    stated in the record.  Written before any rank touches a GPU."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from mini_parallel_amd.synthetic import BGZF_EOF, wgs_genome
+    from oracle import oracle_lib
+    global _POOL_GENOME
+    d, files, plan = c4_layout(args)
+    names = [os.path.basename(p) for p in files]
+    m = _marker_ok(d, names)
+    if m is not None:
+        m["reused"] = True
+        return m
+    import shutil
+    if os.path.isdir(args.c4_dir):  # earlier config-4 datasets of this bench (disk: ~37 GB each)
+        for e in os.listdir(args.c4_dir):
+            if e.startswith(f"l{C4_LANES}x{C4_READS_PER_LANE}_r"):
+                shutil.rmtree(os.path.join(args.c4_dir, e), ignore_errors=True)
+    os.makedirs(os.path.join(d, "pool"), exist_ok=True)
+    oracle_lib.build()
+    oracle_lib.lib()
+    _POOL_GENOME = wgs_genome(C4_SEED, C4_GENOME)
+    _write_reference(os.path.join(d, "reference.fa"), _POOL_GENOME, C4_SEED)
+    S, P = args.c4_segment_reads, args.c4_pool
+    jobs = [(i, S, os.path.join(d, "pool", "seg_%03d.bgz" % i)) for i in range(P)]
+    segs, gen_s = _run_pool(_c4_segment_job, jobs, host_cpus()[2], f"config-4 segment pool ({P} x {S} reads)")
+    _POOL_GENOME = None
+    need = sum(segs[i]["bytes"] for row in plan for i in row)
+    free = shutil.disk_usage(d).free
+    if free < need + (2 << 30):
+        raise RuntimeError(f"config-4 lane files need {need / 1e9:.1f} GB, {args.c4_dir} has {free / 1e9:.1f} GB free")
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=min(16, len(files))) as ex:
+        futs = [ex.submit(_copy_into, fp, [jobs[i][2] for i in row], BGZF_EOF) for fp, row in zip(files, plan)]
+        for k, fu in enumerate(futs):
+            fu.result()
+            print(f"[bench] config-4 lane file {k + 1}/{len(files)} assembled: {time.perf_counter() - t0:.0f} s",
+                  file=sys.stderr, flush=True)
+        sizes = [fu.result() for fu in futs]
+    asm_s = time.perf_counter() - t0
+    expect = {n: {"score": sum(segs[i]["score"] for i in row), "reads": sum(segs[i]["reads"] for i in row),
+                  "bases": sum(segs[i]["bases"] for i in row)} for n, row in zip(names, plan)}
+    m = {"sizes": dict(zip(names, sizes)), "expect": expect, "plan": plan, "segments": segs,
+         "gen_seconds": round(gen_s, 1), "assemble_seconds": round(asm_s, 1),
+         "oracle_thread_seconds": round(sum(s["oracle_s"] for s in segs), 2), "bytes": int(sum(sizes))}
+    _write_marker(d, m)
+    m["reused"] = False
+    return m
+
+
+# config 3 from FASTQ (BASELINE: "1M synthetic 150 bp reads ... affine-gap
+# score + best-cell coord, async FASTQ chunk staging"): 16 lane files of
+# 62,500 reads, every read's (score, end_i, end_j) compared with the oracle.
+C3F_LANES, C3F_RPL, C3F_GENOME, C3F_SEED = 8, 2, 64 << 20, 1003
+
+
+def _c3_file_job(job):
+    """One config-3 lane file: its reads (synthetic._lane_reads, file k),
+    BGZF level 6 + EOF block, and the oracle's affine + best-cell result of
+    every read (one thread) saved beside it."""
+    from mini_parallel_amd.synthetic import _lane_reads, _lane_records, _with_windows, bgzf_compress
+    from oracle import oracle_lib
+    k, n, path = job
+    g = _POOL_GENOME
+    b, pos, rng = _lane_reads(g, k, n, 150, 2.0, C3F_SEED)
+    data = bgzf_compress(_lane_records(b, pos, rng, b"SYN", k // C3F_RPL + 1, C4_QUAL), C4_LEVEL)
+    with open(path, "wb") as f:
+        f.write(data)
+    w = _with_windows(g, b, pos)
+    sc = scoring_of(3)
+    t0 = time.perf_counter()
+    s, i, j, _ = oracle_lib.sw_batch_simd(w.reads, w.read_len, w.wins, w.win_len, threads=1, coords=True,
+                                          **_oracle_kw(sc))
+    dt = time.perf_counter() - t0
+    np.savez(path + ".oracle.npz", score=s, end_i=i, end_j=j)
+    return {"bytes": len(data), "cells": int(w.cells), "reads": int(n), "oracle_s": dt}
+
+
+def c3f_layout(args):
+    n_files = C3F_LANES * C3F_RPL
+    per = args.c3_fastq_reads // n_files
+    d = os.path.join(args.c4_dir, f"c3fastq_{C3F_LANES}x{C3F_RPL}_r{per}_g{C3F_GENOME}_s{C3F_SEED}")
+    return d, [os.path.join(d, n) for n in _lane_names(C3F_LANES, C3F_RPL)], per
+
+
+def ensure_c3f_dataset(args) -> dict:
+    from mini_parallel_amd.synthetic import wgs_genome
+    from oracle import oracle_lib
+    global _POOL_GENOME
+    d, files, per = c3f_layout(args)
+    names = [os.path.basename(p) for p in files]
+    m = _marker_ok(d, names)
+    if m is not None:
+        m["reused"] = True
+        return m
+    os.makedirs(d, exist_ok=True)
+    oracle_lib.build()
+    oracle_lib.lib()
+    _POOL_GENOME = wgs_genome(C3F_SEED, C3F_GENOME)
+    _write_reference(os.path.join(d, "reference.fa"), _POOL_GENOME, C3F_SEED)
+    res, gen_s = _run_pool(_c3_file_job, [(k, per, p) for k, p in enumerate(files)], host_cpus()[2],
+                           f"config-3 lane files ({len(files)} x {per} reads)")
+    _POOL_GENOME = None
+    m = {"sizes": {n: r["bytes"] for n, r in zip(names, res)}, "cells": sum(r["cells"] for r in res),
+         "gen_seconds": round(gen_s, 1), "oracle_thread_seconds": round(sum(r["oracle_s"] for r in res), 2)}
+    _write_marker(d, m)
+    m["reused"] = False
     return m
 
 
@@ -734,51 +939,98 @@ def _standin_file(path):
     return score, reads, bases
 
 
-def leg_config4(job, args):
-    """configs_extra.config4 -- a bounded BASELINE config 4: the 8 lanes x
-    R1/R2 BGZF lane files of ensure_c4_dataset (the full config is 8 x ~50 M
-    reads; this one is 16 files x --c4-reads-per-file), sharded by file over
-    the ranks (rank r: files r, r + N, ...; strong scaling: the dataset is
-    fixed).  Each rank runs the product's --full-wgs driver on its GPU
-    (rustseq_mini, WGS_FILE_SHARD=r/N, MSW_DEVICES=local rank: the GPU lane
-    reader inflates and parses on the GPU, windows cut from the resident
-    genome, score-only kernel, two workers per GPU), as a child process
-    started after the fence.  Per-file (score i64, reads, bases) rows are
-    all-gathered over RCCL; rank 0 checks every file finished, the read
-    count, and file 0's i64 score sum against the oracle."""
-    from mini_parallel_amd import dist as mdist
-    d, files = c4_layout(args)
-    F, R = len(files), args.c4_reads_per_file
-    mine = list(range(job.rank, F, job.world))
-    rows, stats, err, cells = [], [0.0, 0.0, 0.0, 0.0, 0.0], "", 0
-    if job.gpu:
-        import tempfile
-        cli = os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini")
-        wd = tempfile.mkdtemp(prefix=f"msw_c4_r{job.rank}_")
-        env = dict(os.environ, WGS_DATA_DIR=d, WGS_SAMPLE_ID="SYN", WGS_LANES=str(C4_LANES),
-                   WGS_READS_PER_LANE=str(C4_READS_PER_LANE), GPU_CHUNK_SIZE_READS="65536",
-                   WGS_FILE_SHARD=f"{job.rank}/{job.world}", MSW_DEVICES=str(job.local_rank),
-                   WGS_RUN_ID=f"bench_c4_r{job.rank}_{os.getpid()}")
-        rec_path = os.path.join(wd, "rec.json")
-        cmd = [cli, "--full-wgs", "--gpu", "--score-mode", "sw", "--reference", os.path.join(d, "reference.fa"),
-               "--window", str(C4_WINDOW), "--checkpoint-dir", wd, "--json", rec_path, "--num-gpus", "1"]
-        job.fence()
-        t0 = time.perf_counter()
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
-        proc = time.perf_counter() - t0
-        job.fence()
+def _standin_records(path):
+    """--cpu-standin: per-read stand-in records (score, end_i, end_j) of a
+    lane file, a deterministic function of each read (NOT a scorer)."""
+    from mini_parallel_amd.fastq import FastqReader
+    out = []
+    with FastqReader(path) as fq:
+        while True:
+            seqs, lens = fq.next_chunk(4096, stride=256)
+            if len(lens) == 0:
+                break
+            out.append(np.stack([31 * lens.astype(np.int32) + seqs[:, 0], lens.astype(np.int32) - 1,
+                                 seqs[:, 1].astype(np.int32)], axis=1))
+    return np.concatenate(out) if out else np.zeros((0, 3), np.int32)
+
+
+def run_wgs_child(job, d, lanes, rpl, reference, extra_args, tag, timeout_s):
+    """This rank's share of a lane set through the product's --full-wgs
+    driver: rustseq_mini in a child process started after the job fence,
+    lane files rank, rank + N, ... (WGS_FILE_SHARD), GPU = local rank.
+    Returns (record, checkpoint, process seconds, workdir, error text)."""
+    import tempfile
+    cli = os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini")
+    wd = tempfile.mkdtemp(prefix=f"msw_{tag}_r{job.rank}_")
+    env = dict(os.environ, WGS_DATA_DIR=d, WGS_SAMPLE_ID="SYN", WGS_LANES=str(lanes),
+               WGS_READS_PER_LANE=str(rpl), GPU_CHUNK_SIZE_READS="65536",
+               WGS_FILE_SHARD=f"{job.rank}/{job.world}", MSW_DEVICES=str(job.local_rank),
+               WGS_RUN_ID=f"bench_{tag}_r{job.rank}_{os.getpid()}")
+    rec_path = os.path.join(wd, "rec.json")
+    cmd = [cli, "--full-wgs", "--gpu", "--score-mode", "sw", "--reference", reference, "--window", str(C4_WINDOW),
+           "--checkpoint-dir", wd, "--json", rec_path, "--num-gpus", "1"] + [x.replace("{wd}", wd) for x in extra_args]
+    job.fence()
+    t0 = time.perf_counter()
+    err, rec, ck = "", None, None
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
         if r.returncode != 0:
-            err = (r.stdout[-1500:] + r.stderr[-1500:]).strip()
-        else:
+            err = f"rustseq_mini exit {r.returncode}:\n" + (r.stdout[-1500:] + r.stderr[-1500:]).strip()
+    except subprocess.TimeoutExpired as e:
+        err = f"rustseq_mini did not finish in {timeout_s} s: {str(e.stdout or '')[-800:]}"
+    proc = time.perf_counter() - t0
+    job.fence()
+    if not err:
+        try:
             with open(rec_path) as f:
                 rec = json.load(f)
             with open(os.path.join(wd, f"checkpoint_{rec['run_id']}.json")) as f:
                 ck = json.load(f)
+        except (OSError, ValueError, KeyError) as e:
+            err = f"run record unreadable: {e}"
+    if err:
+        print(f"bench.py rank {job.rank}: {tag} leg failed:\n{err}", file=sys.stderr, flush=True)
+    return rec, ck, proc, wd, err
+
+
+def _setup_split(rec):
+    """The CLI's setup phases (max over its workers) as a flat list."""
+    ph = (rec or {}).get("setup_phases") or {}
+    return [float(ph.get(k, 0.0)) for k in SETUP_PHASES]
+
+
+SETUP_PHASES = ("hip_init_ms", "reference_load_ms", "context_ms", "genome_ms", "result_sets_ms", "lane_reader_ms")
+
+
+def leg_config4(job, args):
+    """configs_extra.config4 -- BASELINE config 4 at its stated size: the 16
+    lane files of ensure_c4_dataset (8 lanes x R1/R2 x 25 M reads = 400 M
+    reads), sharded by file over the ranks (rank r: files r, r + N, ...;
+    strong scaling: the dataset is fixed).  Each rank runs the product's
+    --full-wgs driver on its GPU (GPU lane reader inflating and parsing on
+    the GPU, windows cut from the HBM-resident genome, score-only kernel, two
+    workers per GPU).  Per-file (score i64, reads, bases) rows are
+    all-gathered over RCCL; rank 0 checks EVERY file against the oracle's
+    composed segment sums (aligner.rs:183-362)."""
+    from mini_parallel_amd import dist as mdist
+    (bad,) = job.sum([1 if (args._c4_meta or {}).get("error") else 0])  # only rank 0 generated
+    if bad:
+        return None if job.rank else {"error": args._c4_meta["error"], "parity": {"bit_exact": False}}
+    d, files, plan = c4_layout(args)
+    F, R = len(files), args.c4_reads_per_file
+    mine = list(range(job.rank, F, job.world))
+    rows, stats, err, cells = [], [0.0] * 5, "", 0
+    setup = [0.0] * len(SETUP_PHASES)
+    if job.gpu:
+        rec, ck, proc, _, err = run_wgs_child(job, d, C4_LANES, C4_READS_PER_LANE, os.path.join(d, "reference.fa"),
+                                              [], "c4", 900)
+        if not err:
             for fr in ck["files"]:
                 rows.append([files.index(fr["file_path"]), fr["score"], fr["total_reads"], fr["total_bases"],
                              1 if fr["completed"] else 0])
             stats = [rec["wall_ms"], proc * 1e3, rec["setup_ms"], rec["teardown_ms"], rec["kernel_ms"]]
             cells = int(rec["cells"])
+            setup = _setup_split(rec)
     else:
         job.fence()
         t0 = time.perf_counter()
@@ -788,9 +1040,7 @@ def leg_config4(job, args):
         job.fence()
         stats = [proc * 1e3, proc * 1e3, 0.0, 0.0, 0.0]
         cells = sum(rw[3] for rw in rows) * C4_WINDOW
-    if err:
-        print(f"bench.py rank {job.rank}: config-4 leg failed:\n{err}", file=sys.stderr, flush=True)
-    mx = job.max(stats + [stats[2] + stats[0]])
+    mx = job.max(stats + [stats[2] + stats[0]] + setup)
     tot = job.sum([cells, 1 if err else 0])
     flat = np.array(rows, np.int64).reshape(-1)
     (g,) = mdist.gather_results(job.tensor(flat))
@@ -798,46 +1048,196 @@ def leg_config4(job, args):
         return None
     g = g.cpu().numpy().reshape(-1, 5)
     if tot[1]:
-        raise SystemExit("bench.py: the config-4 leg failed on some rank (see stderr)")
+        return {"error": "the config-4 leg failed on some rank (see stderr)", "n_ranks": job.world,
+                "parity": {"bit_exact": False}}
     table = np.zeros((F, 4), np.int64)
     seen = np.zeros(F, np.int64)
     for fi, sc, nr, nb, done in g:
         table[fi] = (sc, nr, nb, done)
         seen[fi] += 1
     reads = int(table[:, 1].sum())
+    with open(os.path.join(d, "DONE.json")) as f:
+        expect = json.load(f)["expect"]
+    bad = []
+    for fi, p in enumerate(files):
+        e = expect[os.path.basename(p)]
+        ok_rb = table[fi, 1] == e["reads"] and table[fi, 2] == e["bases"]
+        ok_sc = (table[fi, 0] == e["score"]) if job.gpu else True
+        if not (ok_rb and ok_sc and table[fi, 3] == 1 and seen[fi] == 1):
+            bad.append(os.path.basename(p))
     par = {"files": F, "files_once": bool((seen == 1).all()), "files_done": int(table[:, 3].sum()),
-           "reads": reads, "reads_expected": F * R}
+           "reads": reads, "reads_expected": F * R, "files_checked": F, "files_mismatched": bad,
+           "check": "every lane file's (score i64, reads, bases) against the sums of its segments' oracle "
+                    "results (oracle/sw_simd.c, each segment scored once when the pool was generated)"}
     if job.gpu:
-        from mini_parallel_amd.synthetic import lane_file_batch
-        from oracle import oracle_lib
-        b = lane_file_batch(0, R, read_len=150, seed=C4_SEED, genome_bases=C4_GENOME)
-        s, _, _, _ = oracle_lib.sw_batch_simd(b.reads, b.read_len, b.wins, b.win_len, threads=host_cpus()[2],
-                                              coords=False)
-        par.update({"checked_file": os.path.basename(files[0]), "oracle_score": int(s.astype(np.int64).sum()),
-                    "gpu_score": int(table[0, 0])})
-        par["bit_exact"] = (par["oracle_score"] == par["gpu_score"] and par["files_once"]
-                            and par["files_done"] == F and reads == F * R)
+        par["gpu_total_score"] = int(table[:, 0].sum())
+        par["oracle_total_score"] = int(sum(expect[os.path.basename(p)]["score"] for p in files))
+        par["bit_exact"] = not bad and reads == F * R
     else:
         want = _standin_file(files[0])
-        par.update({"standin": True, "file0_ok": bool(tuple(table[0, :3]) == want)})
-    wall_ms, proc_ms, setup_ms, tear_ms, kern_ms, setup_wall_ms = mx
+        par.update({"standin": True, "file0_ok": bool(tuple(table[0, :3]) == want), "rows_ok": not bad})
+    wall_ms, proc_ms, setup_ms, tear_ms, kern_ms, setup_wall_ms = mx[:6]
     job_cells = int(tot[0])
-    return {"workload": f"config4 (bounded): {C4_LANES} lanes x {C4_READS_PER_LANE} BGZF lane files x {R} "
-                        f"reads of 150 bp (zlib level {C4_LEVEL}, {C4_QUAL} qualities), {C4_GENOME >> 20} Mbp "
-                        f"HBM-resident genome, window {C4_WINDOW}, linear score sums per file; the full config "
-                        "is 8 x ~50 M reads",
-            "n_ranks": job.world, "scaling": "strong", "files_per_rank": len(mine), "reads": reads,
-            "gcups": round(job_cells / (wall_ms * 1e6), 1),
+    S, P = args.c4_segment_reads, args.c4_pool
+    out = {"workload": f"config4: {C4_LANES} lanes x {C4_READS_PER_LANE} BGZF lane files x {R} reads of 150 bp "
+                       f"= {F * R} reads (zlib level {C4_LEVEL}, {C4_QUAL} qualities), {C4_GENOME >> 20} Mbp "
+                       f"HBM-resident genome, window {C4_WINDOW}, linear score sums per file; each file is "
+                       f"{R // S} segments of {S} reads drawn from a pool of {P} distinct segments (segments repeat)",
+           "n_ranks": job.world, "scaling": "strong", "files_per_rank": len(mine), "reads": reads,
+           "gcups": round(job_cells / (wall_ms * 1e6), 1),
+           "reads_per_s": round(reads / (wall_ms * 1e-3)),
+           "reads_per_s_incl_setup": round(reads / (setup_wall_ms * 1e-3)),
+           "reads_per_s_process": round(reads / (proc_ms * 1e-3)),
+           "wall_ms": round(wall_ms, 1), "setup_ms": round(setup_ms, 1), "teardown_ms": round(tear_ms, 1),
+           "process_wall_ms": round(proc_ms, 1), "max_kernel_ms": round(kern_ms, 1),
+           "setup_phases_ms": {k: round(v, 1) for k, v in zip(SETUP_PHASES, mx[6:])},
+           "timing": "wall_ms = the --full-wgs driver's timed region (workers set up -> last results on the "
+                     "host), max over ranks; setup_ms = contexts, genome upload and reader buffers before it "
+                     "(setup_phases_ms: each phase's max over workers and ranks; hip_init_ms and "
+                     "reference_load_ms come before setup_ms); process_wall_ms = the rank's child process "
+                     "start to exit",
+           "segments": {"pool": P, "segment_reads": S, "segments_per_file": R // S,
+                        "distinct_reads": P * S, "note": "lane files are concatenations of pooled, pre-scored "
+                                                         "segments: reads repeat across and within files"},
+           "gather": "per-file (score i64, reads, bases) rows all-gathered over the process group",
+           "parity": par, "dataset": {k: v for k, v in (args._c4_meta or {}).items() if not k.startswith("_")}}
+    if job.gpu and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline_c4(args)
+    return out
+
+
+def cpu_baseline_c4(args):
+    """configs_extra.config4.cpu_baseline: the SIMD restatement scoring pool
+    segment 0 (its reads against their genome windows, linear, score only)
+    on every CPU this job may use, timed here; plus the per-thread rate of
+    the pool generation's oracle pass (each segment scored on one thread,
+    the workers running side by side).  Scoring only: the CPU inflate and
+    parse of the lane files are not in it."""
+    from mini_parallel_amd.synthetic import _lane_reads, _with_windows, wgs_genome
+    from oracle import oracle_lib
+    g = wgs_genome(C4_SEED, C4_GENOME)
+    b, pos, _ = _lane_reads(g, 0, args.c4_segment_reads, 150, 2.0, C4_SEED, segment=1)
+    w = _with_windows(g, b, pos)
+    _, _, usable = host_cpus()
+    passes, dt, t0 = 0, 0.0, time.perf_counter()
+    while dt < max(1.0, args.cpu_seconds / 4):
+        s, _, _, isa = oracle_lib.sw_batch_simd(w.reads, w.read_len, w.wins, w.win_len, threads=usable, coords=False)
+        passes += 1
+        dt = time.perf_counter() - t0
+    meta = args._c4_meta or {}
+    seg0 = (meta.get("segments") or [{}])[0]
+    thr = meta.get("_segment_rates") or []
+    per_thread = (sum(c for c, _ in thr) / sum(t for _, t in thr) / 1e9) if thr else None
+    gc = passes * w.cells / dt / 1e9
+    return {"value": round(gc, 2), "unit": "GCUPS", "cores": usable, "kind": "port",
+            "reads_per_s": round(passes * w.n_pairs / dt),
+            "sample": f"{passes} pass(es) of oracle/sw_simd.c ({isa}-bit) over pool segment 0 ({w.n_pairs} reads x "
+                      f"300 bp windows, {w.cells} cells, {dt:.1f} s) on {usable} threads",
+            "segment0_score_matches_pool": bool(int(s.astype(np.int64).sum()) == seg0.get("score")),
+            "pool_pass_per_thread_gcups": None if per_thread is None else round(per_thread, 2),
+            "scope": "scoring only (no CPU inflate / parse)"}
+
+
+def leg_config3_fastq(job, args):
+    """configs_extra.config3.fastq -- BASELINE config 3 as stated: 1 M reads
+    in BGZF lane files (16 x 62,500), through the product's --full-wgs
+    driver with --gap-model affine --scores-out (lane loader -> batches in
+    HBM -> affine + best cell -> per-read (score, end_i, end_j) records on
+    the host, aligner.rs:107-178, 269-289, 466-475), sharded by file over the
+    ranks.  Every record is gathered over the process group and rank 0
+    compares all of them with the oracle's."""
+    from mini_parallel_amd import dist as mdist
+    (bad,) = job.sum([1 if (args._c3f_meta or {}).get("error") else 0])  # only rank 0 generated
+    if bad:
+        return None if job.rank else {"error": args._c3f_meta["error"], "parity": {"bit_exact": False}}
+    d, files, per = c3f_layout(args)
+    F = len(files)
+    stats, err, cells, recs, idx = [0.0] * 5, "", 0, [], []
+    setup = [0.0] * len(SETUP_PHASES)
+    if job.gpu:
+        rec, ck, proc, wd, err = run_wgs_child(job, d, C3F_LANES, C3F_RPL, os.path.join(d, "reference.fa"),
+                                               ["--gap-model", "affine", "--scores-out", "{wd}"], "c3f", 600)
+        if not err:
+            for fr in sorted(ck["files"], key=lambda x: files.index(x["file_path"])):
+                fi = files.index(fr["file_path"])
+                raw = np.fromfile(os.path.join(wd, os.path.basename(fr["file_path"]) + ".scores"), np.uint8)
+                r = raw.view([("s", "<i4"), ("i", "<i2"), ("j", "<i2")])
+                recs.append(np.stack([r["s"].astype(np.int32), r["i"].astype(np.int32), r["j"].astype(np.int32)], 1))
+                idx.append([fi, r.shape[0], 1 if fr["completed"] else 0])
+            stats = [rec["wall_ms"], proc * 1e3, rec["setup_ms"], rec["teardown_ms"], rec["kernel_ms"]]
+            cells = int(rec["cells"])
+            setup = _setup_split(rec)
+    else:
+        job.fence()
+        t0 = time.perf_counter()
+        for fi in range(job.rank, F, job.world):
+            r = _standin_records(files[fi])
+            recs.append(r)
+            idx.append([fi, r.shape[0], 1])
+        proc = time.perf_counter() - t0
+        job.fence()
+        stats = [proc * 1e3] * 2 + [0.0] * 3
+        cells = sum(int(r.shape[0]) for r in recs) * C4_WINDOW
+    mx = job.max(stats + [stats[2] + stats[0]] + setup)
+    tot = job.sum([cells, 1 if err else 0])
+    allr = np.concatenate(recs) if recs else np.zeros((0, 3), np.int32)
+    t_s, t_i, t_j = (job.tensor(np.ascontiguousarray(allr[:, c])) for c in range(3))
+    # int16 coordinates ride the gather's int32 wire cast; the per-file index
+    # rows (a different length) are a gather of their own
+    g_s, g_i, g_j = mdist.gather_results(t_s, t_i.to(dtype=_torch().int16), t_j.to(dtype=_torch().int16))
+    (g_idx,) = mdist.gather_results(job.tensor(np.array(idx, np.int64).reshape(-1)))
+    if job.rank != 0:
+        return None
+    if tot[1]:
+        return {"error": "the config-3 FASTQ leg failed on some rank (see stderr)", "parity": {"bit_exact": False}}
+    g_s, g_i, g_j = g_s.cpu().numpy(), g_i.cpu().numpy(), g_j.cpu().numpy()
+    g_idx = g_idx.cpu().numpy().reshape(-1, 3)
+    off, order = 0, {}
+    for fi, n, done in g_idx:
+        order[int(fi)] = (off, int(n), int(done))
+        off += int(n)
+    mism, checked, files_ok = 0, 0, 0
+    for fi, p in enumerate(files):
+        if fi not in order:
+            continue
+        o, n, done = order[fi]
+        files_ok += done
+        if job.gpu:
+            z = np.load(p + ".oracle.npz")
+            want = np.stack([z["score"], z["end_i"], z["end_j"]], 1).astype(np.int64)
+        else:
+            want = _standin_records(p).astype(np.int64)
+        got = np.stack([g_s[o:o + n], g_i[o:o + n], g_j[o:o + n]], 1).astype(np.int64)
+        if got.shape != want.shape:
+            mism += max(n, want.shape[0])
+        else:
+            mism += int((got != want).any(axis=1).sum())
+        checked += n
+    wall_ms, proc_ms, setup_ms, tear_ms, kern_ms, setup_wall_ms = mx[:6]
+    reads = int(g_idx[:, 1].sum()) if g_idx.size else 0
+    return {"workload": f"config3 from FASTQ: {F} BGZF lane files x {per} reads of 150 bp = {F * per} reads, "
+                        f"{C3F_GENOME >> 20} Mbp HBM-resident genome, window {C4_WINDOW}, affine (open 3, extend 1) "
+                        "+ best cell, per-read records (--scores-out)",
+            "n_ranks": job.world, "scaling": "strong", "reads": reads,
+            "gcups_end_to_end": round(int(tot[0]) / (wall_ms * 1e6), 1),
+            "gcups_incl_setup": round(int(tot[0]) / (setup_wall_ms * 1e6), 1),
             "reads_per_s": round(reads / (wall_ms * 1e-3)),
             "reads_per_s_incl_setup": round(reads / (setup_wall_ms * 1e-3)),
-            "reads_per_s_process": round(reads / (proc_ms * 1e-3)),
-            "wall_ms": round(wall_ms, 1), "setup_ms": round(setup_ms, 1), "teardown_ms": round(tear_ms, 1),
-            "process_wall_ms": round(proc_ms, 1), "max_kernel_ms": round(kern_ms, 1),
-            "timing": "wall_ms = the --full-wgs driver's timed region (workers set up -> last results on the "
-                      "host), max over ranks; setup_ms = contexts, genome upload and reader buffers before it; "
-                      "process_wall_ms = the rank's child process start to exit (HIP init, setup, teardown)",
-            "gather": "per-file (score i64, reads, bases) rows all-gathered over RCCL",
-            "parity": par, "dataset_gen_seconds": args._c4_gen_seconds}
+            "wall_ms": round(wall_ms, 1), "setup_ms": round(setup_ms, 1), "process_wall_ms": round(proc_ms, 1),
+            "max_kernel_ms": round(kern_ms, 1),
+            "setup_phases_ms": {k: round(v, 1) for k, v in zip(SETUP_PHASES, mx[6:])},
+            "parity": {"records_checked": checked, "records_expected": F * per, "mismatches": mism,
+                       "files_done": files_ok,
+                       "bit_exact": mism == 0 and checked == F * per and files_ok == F,
+                       "check": "every read's (score, end_i, end_j) against the oracle (oracle/sw_simd.c, "
+                                "affine + best cell), records gathered over the process group",
+                       **({"standin": True} if not job.gpu else {})},
+            "dataset": {k: v for k, v in (args._c3f_meta or {}).items() if not k.startswith("_")}}
+
+
+def _torch():
+    import torch
+    return torch
 
 
 # ---------------------------------------------------------------------------
@@ -853,16 +1253,16 @@ def main(argv=None):
     else:
         world = args.gpus or 1
         if world > 1:
-            if 4 in extras and (args.cpu_standin or visible_gpus() >= world):
-                ensure_c4_dataset(args)  # before the ranks start
+            if args.cpu_standin or visible_gpus() >= world:
+                prepare_datasets(args, extras)  # before the ranks start (they reuse it)
             return launch_ranks(args, argv)
     rank = int(os.environ.get("RANK", 0))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     gpu = not args.cpu_standin
-    args._c4_gen_seconds = None
-    if 4 in extras and rank == 0:
+    args._c4_meta = args._c3f_meta = None
+    if rank == 0:
         # before anything touches the GPU; the other ranks wait in init_process_group
-        args._c4_gen_seconds = ensure_c4_dataset(args).get("gen_seconds")
+        prepare_datasets(args, extras)
 
     import datetime
 
@@ -876,9 +1276,13 @@ def main(argv=None):
             print(f"bench.py: rank {rank} needs GPU {local_rank} of {local_world} but only {have} GPU(s) are visible",
                   file=sys.stderr, flush=True)
             return 3
-    if world > 1:
-        dist.init_process_group("nccl" if gpu else "gloo", init_method="env://",
-                                timeout=datetime.timedelta(minutes=30))
+        torch.cuda.set_device(local_rank)
+    # A process group at every N, N = 1 included: the gathers, max / sum
+    # reductions and barriers of every leg run through RCCL ("nccl") on the
+    # GPUs whatever the GPU count (gloo for --cpu-standin).
+    pg_init = "env://" if "WORLD_SIZE" in os.environ else f"tcp://127.0.0.1:{_free_port()}"
+    dist.init_process_group("nccl" if gpu else "gloo", init_method=pg_init, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(minutes=30))
     from mini_parallel_amd import dist as mdist
     from mini_parallel_amd.synthetic import config_shard
 
@@ -893,7 +1297,6 @@ def main(argv=None):
 
     ctx = None
     if gpu:
-        torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
         from mini_parallel_amd import Context
         ctx = Context(local_rank)
@@ -947,6 +1350,10 @@ def main(argv=None):
             continue
         if c in (3, 5):
             extra[f"config{c}"] = leg_pairs(job, ctx, c, args)
+            if c == 3 and args.c3_fastq_reads > 0:
+                r = leg_config3_fastq(job, args)  # BASELINE config 3 from lane files
+                if rank == 0:
+                    extra["config3"]["fastq"] = r
         elif c == 4:
             extra["config4"] = leg_config4(job, args)
 
@@ -1022,16 +1429,44 @@ def main(argv=None):
             "pcie_inclusive": pcie,
             "cut_windows_roofline": cut,
             "gathered_scores": gathered,
+            "collectives": {"backend": mdist.backend(), "world": world, "calls_rank0": dict(mdist.CALLS),
+                            "note": "every max / sum / gather / barrier of the run goes through this process "
+                                    "group (RCCL = the nccl backend on ROCm), at N = 1 too"},
         }
         if not gpu:
             line["standin"] = True
             line["standin_scores"] = g_score.tolist() if g_score.size <= 100_000 else None
         print(json.dumps(line), flush=True)
 
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    dist.barrier()
+    dist.destroy_process_group()
     return 0
+
+
+def prepare_datasets(args, extras):
+    """The lane sets of the FASTQ legs (config 4, config 3 from FASTQ), written
+    once before any rank touches a GPU.  A failure (e.g. no disk space) is
+    kept as the leg's error instead of ending the bench."""
+    args._c4_meta = args._c3f_meta = None
+    if 4 in extras:
+        try:
+            args._c4_meta = ensure_c4_dataset(args)
+        except (OSError, RuntimeError) as e:
+            args._c4_meta = {"error": f"config-4 dataset: {e}"}
+    if 3 in extras and args.c3_fastq_reads > 0:
+        try:
+            args._c3f_meta = ensure_c3f_dataset(args)
+        except (OSError, RuntimeError) as e:
+            args._c3f_meta = {"error": f"config-3 FASTQ dataset: {e}"}
+    for m in (args._c4_meta, args._c3f_meta):  # the record keeps the summary, not the per-file tables
+        if m and "error" not in m:
+            for k in ("expect", "plan", "sizes"):
+                m.pop(k, None)
+            segs = m.pop("segments", None)
+            if segs:
+                m["segments"] = [{k: s[k] for k in ("segment", "reads", "score", "bytes")} for s in segs[:4]]
+                m["segments_total"] = len(segs)
+                m["_segment_rates"] = [(s["cells"], s["oracle_s"]) for s in segs]
 
 
 def load_pmc_traffic(key: str):

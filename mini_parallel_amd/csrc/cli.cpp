@@ -548,6 +548,11 @@ struct WgsReport {
     bool gpu_inflate = false;      // lane files inflated and parsed on the GPUs
     double setup_ms = 0;           // worker setup before the clock started (contexts, genome, buffers)
     double teardown_ms = 0;        // release after the last results, outside the clock
+    // setup split (JSON "setup_phases", each phase's max over the workers):
+    // reference_load before setup_ms; context / genome upload / result sets /
+    // lane reader inside it (workers run them side by side); hip_init is
+    // filled in by main (the first HIP call, before any of these)
+    double reference_load_ms = 0, context_ms = 0, genome_ms = 0, result_sets_ms = 0, lane_reader_ms = 0;
     unsigned long long gz_in = 0, gz_out = 0;  // compressed / inflated bytes (GPU lane reader)
 };
 
@@ -579,14 +584,35 @@ std::vector<Device> worker_devices(const std::vector<Device>& devs, int n) {
     return pool;
 }
 
+// files: this process's lane files; gidx[i]: file i's index in the whole lane
+// set (WGS_FILE_SHARD takes a subset), used for messages and the checkpoint.
 WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const std::vector<std::string>& files,
-                       Checkpoint& ckpt) {
+                       const std::vector<size_t>& gidx, size_t n_lane_files, Checkpoint& ckpt) {
     const uint64_t chunk = get_chunk_size_reads();
     const bool sw = a.score_mode == "sw";
     std::string genome;
+    double ref_ms = 0;
+    std::mutex setup_mu;
+    double ph_ctx = 0, ph_gen = 0, ph_res = 0, ph_reader = 0;  // max over workers
+    auto setup_phase = [&](double c, double g, double r, double rd) {
+        std::lock_guard<std::mutex> lk(setup_mu);
+        ph_ctx = std::max(ph_ctx, c);
+        ph_gen = std::max(ph_gen, g);
+        ph_res = std::max(ph_res, r);
+        ph_reader = std::max(ph_reader, rd);
+    };
+    auto report_setup = [&](WgsReport& rep) {
+        rep.reference_load_ms = ref_ms;
+        rep.context_ms = ph_ctx;
+        rep.genome_ms = ph_gen;
+        rep.result_sets_ms = ph_res;
+        rep.lane_reader_ms = ph_reader;
+    };
     if (sw) {
         if (a.reference.empty()) die("error: --score-mode sw with --full-wgs needs --reference <FASTA>");
+        const auto t_ref = Clock::now();
         genome = load_fasta(a.reference);
+        ref_ms = ms_since(t_ref);
         printf("Loaded reference: %zu bases\n", genome.size());
     }
     const int ngpu = (int)devices.size();  // already worker_devices(): one worker per entry
@@ -596,10 +622,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     for (size_t i = 0; i < files.size(); ++i) {
         st[i].reset(new FileState());
         st[i]->path = files[i];
-        auto it = ckpt.files.find(i);
+        auto it = ckpt.files.find(gidx[i]);
         if (it != ckpt.files.end() && it->second.completed && it->second.file_path == files[i]) {
-            printf("  Skipping completed file %zu/%zu: %s (score %lld)\n", i + 1, files.size(), files[i].c_str(),
-                   it->second.score);
+            printf("  Skipping completed file %zu/%zu: %s (score %lld)\n", gidx[i] + 1, n_lane_files,
+                   files[i].c_str(), it->second.score);
         } else {
             todo.push_back(i);
         }
@@ -638,16 +664,16 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         }
         FileCheckpoint c;
         c.file_path = f.path;
-        c.file_index = fi;
+        c.file_index = gidx[fi];
         c.score = f.score.load();
         c.processing_time_ms = f.ms;
         c.total_bases = f.bases.load();
         c.total_reads = f.reads.load();
         c.completed = !f.failed.load();
         std::lock_guard<std::mutex> lk(ck_mu);
-        ckpt.files[fi] = c;
+        ckpt.files[gidx[fi]] = c;
         ckpt.save();
-        printf("  File %zu done: %s score=%lld reads=%llu bases=%llu time=%.2fs%s\n", fi + 1, f.path.c_str(),
+        printf("  File %zu done: %s score=%lld reads=%llu bases=%llu time=%.2fs%s\n", gidx[fi] + 1, f.path.c_str(),
                c.score, c.total_reads, c.total_bases, f.ms / 1000.0, c.completed ? "" : " (FAILED)");
         fflush(stdout);
     };
@@ -676,7 +702,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         for (int wi = 0; wi < nworkers; ++wi) {
             workers.emplace_back([&, wi]() {
                 const int gi = wi % ngpu;
-                static const bool strace = getenv("MSW_SETUP_TRACE") != nullptr;  // setup phases to stderr
                 const auto ts0 = Clock::now();
                 Ctx ctx(devices[gi].ordinal);
                 const double t_ctx = ms_since(ts0);
@@ -764,10 +789,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 const double t_res = ms_since(ts0);
                 if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
                     die(std::string("GPU lane reader: ") + msw_last_error());
-                if (strace)
-                    fprintf(stderr, "[setup] worker %d: context %.1f ms, genome %.1f ms, result sets %.1f ms, "
-                                    "lane reader %.1f ms\n", wi, t_ctx, t_gen - t_ctx, t_res - t_gen,
-                            ms_since(ts0) - t_res);
+                setup_phase(t_ctx, t_gen - t_ctx, t_res - t_gen, ms_since(ts0) - t_res);
                 // the reader's stats of the file it just finished
                 auto reader_done = [&](size_t fi) {
                     uint64_t bi = 0, bo = 0;
@@ -796,7 +818,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                             f.scores_fd = open(out.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
                             if (f.scores_fd < 0) die("error: cannot create " + out);
                         }
-                        printf("  Processing file %zu/%zu: %s (GPU inflate)\n", fi + 1, files.size(), f.path.c_str());
+                        printf("  Processing file %zu/%zu: %s (GPU inflate)\n", gidx[fi] + 1, n_lane_files,
+                               f.path.c_str());
                         fflush(stdout);
                         if (msw_gfastq_reset(gr, f.path.c_str()) != MSW_OK) {
                             f.error = msw_last_error();
@@ -880,6 +903,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         for (size_t fi : todo) finish_file(fi);
         WgsReport rep;
         rep.setup_ms = std::chrono::duration<double, std::milli>(t_all - t_setup).count();
+        report_setup(rep);
         rep.gz_in = gz_in.load();
         rep.gz_out = gz_out.load();
         wall_and_teardown(rep);
@@ -890,7 +914,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         for (int wi = 0; wi < nworkers; ++wi) rep.gpu_dev.push_back(devices[wi % ngpu].ordinal);
         rep.gpu_inflate = true;
         for (size_t i = 0; i < files.size(); ++i)
-            if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
+            if (ckpt.files.count(gidx[i])) rep.results.push_back(ckpt.files[gidx[i]]);
         return rep;
     }
 
@@ -928,7 +952,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     f.scores_fd = open(out.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
                     if (f.scores_fd < 0) die("error: cannot create " + out);
                 }
-                printf("  Processing file %zu/%zu: %s\n", fi + 1, files.size(), f.path.c_str());
+                printf("  Processing file %zu/%zu: %s\n", gidx[fi] + 1, n_lane_files, f.path.c_str());
                 fflush(stdout);
                 msw_fastq* fq = nullptr;
                 if (msw_fastq_open(f.path.c_str(), &fq) != MSW_OK) {
@@ -991,13 +1015,16 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     std::vector<std::thread> workers;
     for (int g = 0; g < ngpu; ++g) {
         workers.emplace_back([&, g]() {
+            const auto ts0 = Clock::now();
             Ctx ctx(devices[g].ordinal);
+            const double t_ctx = ms_since(ts0);
             const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
             // sw mode: the reference genome lives in this GPU's HBM; a chunk
             // ships reads + window positions, windows are cut on the GPU.
             msw_genome* gen = nullptr;
             if (sw && msw_genome_create(ctx.h, (const uint8_t*)genome.data(), genome.size(), &gen) != MSW_OK)
                 die(std::string("GPU genome upload error: ") + msw_last_error());
+            setup_phase(t_ctx, ms_since(ts0) - t_ctx, 0.0, 0.0);
             gate.arrive();
             // Up to three chunks in flight (msw_align_reads_async; msw_wait on the
             // oldest ticket before a fourth is staged): the context's three
@@ -1121,6 +1148,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     for (size_t fi : todo) finish_file(fi);  // no-op for files already finished
     WgsReport rep;
     rep.setup_ms = std::chrono::duration<double, std::milli>(t_all - t_setup).count();
+    report_setup(rep);
     wall_and_teardown(rep);
     rep.cells = cells.load();
     rep.readers = nreaders;
@@ -1128,7 +1156,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     rep.gpu = gstats;
     for (const Device& d : devices) rep.gpu_dev.push_back(d.ordinal);
     for (size_t i = 0; i < files.size(); ++i)
-        if (ckpt.files.count(i)) rep.results.push_back(ckpt.files[i]);
+        if (ckpt.files.count(gidx[i])) rep.results.push_back(ckpt.files[gidx[i]]);
     return rep;
 }
 
@@ -1161,7 +1189,9 @@ void write_json(const std::string& path, const std::string& body) {
 int main(int argc, char** argv) {
     load_dotenv();
     const Args a = parse_args(argc, argv);
-    const auto devices = get_gpu_devices();
+    const auto t_hip = Clock::now();
+    const auto devices = get_gpu_devices();  // the first HIP call: runtime init
+    const double hip_init_ms = ms_since(t_hip);
     printf("Detecting system information...\n");
     for (const auto& d : devices) printf("  GPU %d: %s (%.1f GB)\n", d.ordinal, d.name.c_str(), d.memory_gb);
     if (devices.empty()) printf("  No GPU detected\n");
@@ -1181,6 +1211,9 @@ int main(int argc, char** argv) {
                 snprintf(name, sizeof(name), "%s/%s_L%03d_R%d_001.fastq.gz", dir.c_str(), sample.c_str(), lane, r);
                 files.push_back(name);
             }
+        const size_t n_lane_files = files.size();
+        std::vector<size_t> gidx(files.size());
+        for (size_t i = 0; i < gidx.size(); ++i) gidx[i] = i;
         // WGS_FILE_SHARD=r/N: this process takes lane files r, r+N, r+2N, ...
         // (one process per GPU, e.g. bench.py's config-4 leg under
         // torch.distributed.run; the reference has no multi-GPU path, gpu.rs:117,125)
@@ -1191,8 +1224,13 @@ int main(int argc, char** argv) {
             if (sscanf(shard.c_str(), "%d/%d%c", &r, &n, &tail) != 2 || n < 1 || r < 0 || r >= n)
                 die("error: WGS_FILE_SHARD must be r/N with 0 <= r < N, got '" + shard + "'");
             std::vector<std::string> mine;
-            for (size_t i = (size_t)r; i < files.size(); i += (size_t)n) mine.push_back(files[i]);
+            std::vector<size_t> mine_idx;
+            for (size_t i = (size_t)r; i < files.size(); i += (size_t)n) {
+                mine.push_back(files[i]);
+                mine_idx.push_back(i);
+            }
             files.swap(mine);
+            gidx.swap(mine_idx);
             printf("File shard %d/%d: %zu lane file(s)\n", r, n, files.size());
         }
         Checkpoint ck;
@@ -1201,7 +1239,7 @@ int main(int argc, char** argv) {
         ck.total_files = files.size();
         if (ck.load()) printf("Resuming run %s from %s\n", ck.run_id.c_str(), ck.path.c_str());
         const std::vector<Device> workers = worker_devices(devices, a.num_gpus);
-        const WgsReport rep = run_full_wgs(a, workers, files, ck);
+        const WgsReport rep = run_full_wgs(a, workers, files, gidx, n_lane_files, ck);
         long long total = 0;
         unsigned long long reads = 0, bases = 0;
         bool all_ok = true;
@@ -1281,7 +1319,11 @@ int main(int argc, char** argv) {
           << ", \"kernel_ms\": " << kmax << ", \"gpu_busy_fraction\": " << busy
           << ", \"alg_bytes\": " << alg << ", \"hbm_gbps\": " << hbm_gbps
           << ", \"roofline_fraction_hbm\": " << frac_hbm << ", \"roofline_fraction_valu\": " << frac_valu
-          << ", \"gpu_inflate\": " << (rep.gpu_inflate ? "true" : "false") << ", \"setup_ms\": " << rep.setup_ms << ", \"teardown_ms\": " << rep.teardown_ms
+          << ", \"gpu_inflate\": " << (rep.gpu_inflate ? "true" : "false") << ", \"setup_ms\": " << rep.setup_ms
+          << ", \"setup_phases\": {\"hip_init_ms\": " << hip_init_ms << ", \"reference_load_ms\": " << rep.reference_load_ms
+          << ", \"context_ms\": " << rep.context_ms << ", \"genome_ms\": " << rep.genome_ms
+          << ", \"result_sets_ms\": " << rep.result_sets_ms << ", \"lane_reader_ms\": " << rep.lane_reader_ms << "}"
+          << ", \"teardown_ms\": " << rep.teardown_ms
           << ", \"inflate_bytes_in\": " << rep.gz_in << ", \"inflate_bytes_out\": " << rep.gz_out
           << ", \"reads_per_second\": " << reads / secs << "}\n";
         write_json(a.json, j.str());

@@ -20,8 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_json_line(tmp_path):
     cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--pairs", "2000",
            "--cpu-seconds", "1", "--no-pcie", "--c3-pairs", "20000", "--c5-pairs", "10000",
-           "--c4-reads-per-file", "20000", "--c4-dir", str(tmp_path / "c4")]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+           "--c4-reads-per-file", "20000", "--c4-segment-reads", "10000", "--c4-pool", "3",
+           "--c3-fastq-reads", "16000", "--c4-dir", str(tmp_path / "c4")]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.strip().splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -59,7 +60,25 @@ def test_bench_json_line(tmp_path):
     assert h["equal_to_hbm_resident_run"] is True and h["value"] > 0 and h["chunk_pairs"] > 0
     c4 = ex["config4"]
     assert c4["parity"]["bit_exact"] is True and c4["reads"] == 16 * 20000
+    assert c4["parity"]["files_checked"] == 16 and c4["parity"]["files_mismatched"] == []
     assert c4["reads_per_s"] >= c4["reads_per_s_incl_setup"] > 0 and c4["setup_ms"] > 0
+    assert c4["setup_phases_ms"]["context_ms"] > 0 and c4["setup_phases_ms"]["hip_init_ms"] > 0
+    assert c4["segments"]["segments_per_file"] == 2 and c4["segments"]["pool"] == 3
+    # BASELINE config 3 from lane files: every per-read record against the oracle
+    f3 = ex["config3"]["fastq"]
+    assert f3["parity"]["bit_exact"] is True and f3["parity"]["records_checked"] == 16000
+    assert f3["reads"] == 16000 and f3["reads_per_s"] > 0 and f3["setup_ms"] > 0
+    # CPU baselines of the other configs' own work (BASELINE.md's plan)
+    for leg in (ex["config3"], ex["config4"], ex["config5"]):
+        cb = leg["cpu_baseline"]
+        assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"], cb
+    assert ex["config3"]["parity"]["rank0_cpu_sample"]["bit_exact"] is True
+    # every max / sum / gather of the run went through RCCL, at N = 1 too
+    col = d["collectives"]
+    assert col["backend"] == "nccl" and col["world"] == 1
+    for k in ("all_reduce_max:float64", "all_reduce_sum:int64", "all_gather:int64", "all_gather:int32",
+              "all_gather:int16->int32"):
+        assert col["calls_rank0"].get(k, 0) >= 1, (k, col)
 
 
 @pytest.mark.gpu

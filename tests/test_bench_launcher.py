@@ -80,7 +80,8 @@ def test_single_rank_standin():
 
 
 EXTRA = ["--cpu-standin", "--steps", "1", "--warmup", "0", "--pairs", "1000", "--cpu-seconds", "0", "--no-pcie",
-         "--extra-configs", "3,4,5", "--c3-pairs", "1500", "--c5-pairs", "1300", "--c4-reads-per-file", "120"]
+         "--extra-configs", "3,4,5", "--c3-pairs", "1500", "--c5-pairs", "1300", "--c4-reads-per-file", "120",
+         "--c4-segment-reads", "40", "--c4-pool", "5", "--c3-fastq-reads", "320"]
 
 
 def _check_extras(d, world):
@@ -97,8 +98,14 @@ def _check_extras(d, world):
     assert c4["n_ranks"] == world and c4["files_per_rank"] == 16 // world and c4["scaling"] == "strong"
     p = c4["parity"]
     assert p["files_once"] and p["files_done"] == 16 and p["reads"] == p["reads_expected"] == 16 * 120
-    assert p["file0_ok"] is True
+    assert p["file0_ok"] is True and p["rows_ok"] is True and p["files_checked"] == 16
     assert c4["reads_per_s"] > 0 and c4["gcups"] > 0
+    assert c4["segments"] == {**c4["segments"], "pool": 5, "segment_reads": 40, "segments_per_file": 3}
+    f3 = ex["config3"]["fastq"]  # per-read records of 16 lane files, gathered in file order
+    assert f3["n_ranks"] == world and f3["reads"] == 320
+    assert f3["parity"]["bit_exact"] is True and f3["parity"]["records_checked"] == 320
+    col = d["collectives"]
+    assert col["backend"] == "gloo" and col["world"] == world and col["calls_rank0"]["all_gather:int16->int32"] >= 1
 
 
 @pytest.mark.parametrize("launch", ["self", "torchrun"])
