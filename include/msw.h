@@ -233,9 +233,11 @@ int msw_fence_wait(msw_ctx* ctx, uint64_t fence);
 /* Counters of the host-batch calls (msw_align_batch*, msw_align_reads*) on a
  * context, for run records (the reference's BenchmarkResult,
  * tools/benchmark.rs:17-34, reports only wall-clock rates):
- * kernel_ms = GPU time of the scoring launches (HIP events on the compute
- * stream around each chunk's launch, added when the chunk is drained; and
- * of msw_align_reads_device launches, added when they have finished),
+ * kernel_ms = GPU time covered by the scoring launches: the union of their
+ * [start, end] intervals (HIP events around each chunk's launch on its
+ * compute stream -- a multi-chunk call alternates two compute streams, whose
+ * launches overlap -- added when the chunk is drained; and around
+ * msw_align_reads_device launches, added when they have finished),
  * alg_bytes = read + window bytes + 4 B score (+ 4 B coordinates) per pair,
  * the kernel's algorithmic HBM traffic.  reset != 0 zeroes them after the copy. */
 typedef struct {

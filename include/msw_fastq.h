@@ -84,7 +84,12 @@ int msw_is_bgzf(const char* path);
  * max_reads: batch size (device slabs for two batches are allocated);
  * span_bytes: decompressed bytes inflated and parsed per step (0 = default
  * 1 GiB, env MSW_GFASTQ_SPAN_MB).  path may be NULL: the buffers are
- * allocated now and msw_gfastq_reset names the first file. */
+ * allocated now and msw_gfastq_reset names the first file.
+ * A lane file must not be modified or truncated while a reader has it open:
+ * its page-cache pages are mapped (MAP_SHARED) and DMA'd in place.  A file
+ * found shorter than when it was opened is reported (MSW_E_INVALID) at the
+ * next span; one truncated while a span's member headers are being indexed
+ * can raise SIGBUS.  MSW_GZ_NO_MAP=1 reads through pread copies instead. */
 int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64_t max_reads, int want_pos,
                     uint64_t span_bytes, msw_gfastq** out);
 /* The next batch, enqueued on `stream` (a hipStream_t; NULL = the context's

@@ -696,7 +696,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         std::vector<std::thread> workers;
         // two workers (contexts) per GPU by default: one file's inflate and
         // host reads overlap the other's scoring
-        const int per_gpu = std::max(1, atoi(env_or("MSW_GFASTQ_WORKERS_PER_GPU", "2").c_str()));
+        // (three or four workers per GPU measured slower: DESIGN.md 5)
+        const int per_gpu = 2;
         const int nworkers = ngpu * per_gpu;
         gstats.assign((size_t)nworkers, msw_stats_t{});
         for (int wi = 0; wi < nworkers; ++wi) {
@@ -920,14 +921,13 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
 
     // Readers: one thread per lane file in flight (a gzip stream inflates on
     // one core; zlib gives ~0.5-0.75 M reads/s per thread, far below what one
-    // GPU scores, so the host side wants every file open at once).  Default
-    // min(files, MSW_HOST_THREADS) -- the CPUs this process may use
-    // (usable_cpus()) -- or MSW_READERS.
+    // GPU scores, so the host side wants every file open at once):
+    // min(files, MSW_HOST_THREADS), by default the CPUs this process may use
+    // (usable_cpus()).
     std::atomic<size_t> next_file{0};
     const int host_threads =
         std::max(1, atoi(env_or("MSW_HOST_THREADS", std::to_string(usable_cpus())).c_str()));
-    const int want_readers = std::max(1, atoi(env_or("MSW_READERS", std::to_string(host_threads).c_str()).c_str()));
-    const int nreaders = std::max(1, std::min<int>((int)todo.size(), std::max(want_readers, 2 * ngpu)));
+    const int nreaders = std::max(1, std::min<int>((int)todo.size(), std::max(host_threads, 2 * ngpu)));
     // Fewer files than the CPU share: BGZF blocks of one file inflate on
     // several threads (msw_fastq.cpp; MSW_INFLATE_THREADS overrides).
     if (!getenv("MSW_INFLATE_THREADS")) {
@@ -1300,7 +1300,10 @@ int main(int argc, char** argv) {
                                                             : (coords ? 10389.5 : 16418.2);
         const double frac_hbm = ng ? hbm_gbps / (8000.0 * ng) : 0.0;
         const double frac_valu = ng && sw_mode ? gcups / (valu_ceiling * ng) : 0.0;
-        const double busy = ng && rep.wall_ms > 0 ? ksum / (ng * rep.wall_ms) : 0.0;
+        // Scoring time per GPU over the wall: each worker's kernel_ms is the
+        // union of its own launches, but two workers on one GPU overlap, so
+        // their sum can exceed the wall -- capped at 1 (an upper bound then).
+        const double busy = ng && rep.wall_ms > 0 ? std::min(1.0, ksum / (ng * rep.wall_ms)) : 0.0;
         std::ostringstream j;
         j << "{\"timestamp\": \"" << ts << "\", \"run_id\": \"" << ck.run_id << "\", \"mode\": \"full_wgs\""
           << ", \"score_mode\": \"" << a.score_mode << "\", \"files_processed\": " << rep.results.size()

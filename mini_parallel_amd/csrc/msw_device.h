@@ -85,17 +85,10 @@ __device__ __forceinline__ uint32_t f16_to_score(uint32_t bits) {
 
 // Score tracking max (opaque so the compiler keeps one op per two rows
 // instead of re-associating into a tree).
-#ifndef MSW_TRACK_ASM
-#define MSW_TRACK_ASM 1
-#endif
 __device__ __forceinline__ uint32_t track_max3(uint32_t best, uint32_t a, uint32_t b) {
-#if MSW_TRACK_ASM
     uint32_t d;
     asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(best), "v"(a), "v"(b));
     return d;
-#else
-    return pk_max3(best, a, b);
-#endif
 }
 
 // Hand-off from lane l-1: DPP wave_shr:1 over the whole wave (lane 0 reads 0
@@ -190,11 +183,7 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 // Wave-wide max of non-negative values, uniform result: DPP row_shr 1/2/4/8
 // (row maxima in lane 15 of each row), row_bcast 15/31, readlane 63 -- six
 // VALU ops instead of six dependent ds_bpermute round trips (__shfl_xor).
-#ifndef MSW_DPP_WAVE_MAX
-#define MSW_DPP_WAVE_MAX 1
-#endif
 __device__ __forceinline__ int wave_max_nonneg(int v) {
-#if MSW_DPP_WAVE_MAX
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true));   // row_shr:1
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true));   // row_shr:2
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true));   // row_shr:4
@@ -202,9 +191,6 @@ __device__ __forceinline__ int wave_max_nonneg(int v) {
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
-#else
-    return __builtin_amdgcn_readfirstlane(wave_max_i32(v));
-#endif
 }
 
 __device__ __forceinline__ uint32_t wcode(uint32_t byte, bool valid, uint32_t shift) {
@@ -613,36 +599,13 @@ __device__ __forceinline__ uint32_t sel_round(const PairMeta& q, uint32_t* strea
 // or faster with 0 (linear + coords 66.4 vs 67.6, affine + coords 97.0 vs 111).
 // Prologue order (profiles/r02/ab/): window loads issued
 // with the read loads, before the wave waits on the pair lengths.
-#ifndef MSW_EARLY_WIN_LOADS
-#define MSW_EARLY_WIN_LOADS 1
-#endif
 // Explicitly scheduled f16 loops of the pairs layout (see sw_body), per
 // scoring kind.  MI355X, tools/sched_ab.sh (10k pairs = one wave per SIMD /
 // 65k-200k pairs), explicit vs hipcc's schedule: linear 46.0 vs 48.1 us /
 // 227 vs 231 us, linear + coords 69.5 vs 77.2 / 347 vs 354, affine + coords
 // 102.9 vs 103.4 / 1585 vs 1594 (200k); affine score-only is faster with
 // hipcc's own schedule at 10k (81.1 vs 85.4, equal at 65k), so it keeps it.
-#ifndef MSW_EXPLICIT_SCHED
-#define MSW_EXPLICIT_SCHED 1
-#endif
-#ifndef MSW_EXPLICIT_AFF
-#define MSW_EXPLICIT_AFF 0
-#endif
-constexpr bool explicit_sched(bool affine, bool coords) {
-    return MSW_EXPLICIT_SCHED && (!affine || coords || MSW_EXPLICIT_AFF);
-}
-#ifndef MSW_PERM_LEAD_LIN
-#define MSW_PERM_LEAD_LIN 2
-#endif
-#ifndef MSW_PERM_LEAD_LIN_COORDS
-#define MSW_PERM_LEAD_LIN_COORDS 0
-#endif
-#ifndef MSW_PERM_LEAD_AFF
-#define MSW_PERM_LEAD_AFF 0
-#endif
-#ifndef MSW_PERM_LEAD_AFF_COORDS
-#define MSW_PERM_LEAD_AFF_COORDS 0
-#endif
+constexpr bool explicit_sched(bool affine, bool coords) { return !affine || coords; }
 // Wavefront steps per loop iteration, per variant (2 or 4; 4 halves the
 // LDS-address adds and avoids rotating the prefetched window words), and
 // whether an odd KR's last row is folded into the score two steps at a time
@@ -650,35 +613,9 @@ constexpr bool explicit_sched(bool affine, bool coords) {
 // (10k / 65k pairs): 4 steps -- linear 9.00 -> 9.25 / 12.20 -> 12.61 TCUPS,
 // affine 4.97 -> 5.48 / 7.08 -> 7.17; with best-cell keys it loses (linear +
 // coords 6.77 -> 6.03, affine + coords 4.64 -> 3.97 at 10k), so those keep 2.
-#ifndef MSW_STEP_UNROLL_LIN
-#define MSW_STEP_UNROLL_LIN 4
-#endif
-#ifndef MSW_STEP_UNROLL_LIN_COORDS
-#define MSW_STEP_UNROLL_LIN_COORDS 2
-#endif
-#ifndef MSW_STEP_UNROLL_AFF
-#define MSW_STEP_UNROLL_AFF 4
-#endif
-#ifndef MSW_STEP_UNROLL_AFF_COORDS
-#define MSW_STEP_UNROLL_AFF_COORDS 2
-#endif
-#ifndef MSW_FOLD_PAIR
-#define MSW_FOLD_PAIR 1
-#endif
-constexpr int step_unroll(bool affine, bool coords) {
-    return affine ? (coords ? MSW_STEP_UNROLL_AFF_COORDS : MSW_STEP_UNROLL_AFF)
-                  : (coords ? MSW_STEP_UNROLL_LIN_COORDS : MSW_STEP_UNROLL_LIN);
-}
-static_assert(step_unroll(false, false) % 2 == 0 && step_unroll(false, false) <= 4 &&
-                  step_unroll(false, true) % 2 == 0 && step_unroll(false, true) <= 4 &&
-                  step_unroll(true, false) % 2 == 0 && step_unroll(true, false) <= 4 &&
-                  step_unroll(true, true) % 2 == 0 && step_unroll(true, true) <= 4,
-              "steps per iteration are 2 or 4");
-
-constexpr int perm_lead(bool affine, bool coords) {
-    return affine ? (coords ? MSW_PERM_LEAD_AFF_COORDS : MSW_PERM_LEAD_AFF)
-                  : (coords ? MSW_PERM_LEAD_LIN_COORDS : MSW_PERM_LEAD_LIN);
-}
+// An odd KR's last row is folded into the score two steps at a time.
+constexpr int step_unroll(bool /*affine*/, bool coords) { return coords ? 2 : 4; }
+constexpr int perm_lead(bool affine, bool coords) { return !affine && !coords ? 2 : 0; }
 
 template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
 __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint32_t* lds, uint64_t& t_loop) {
@@ -704,9 +641,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     load_read_bytes<KR, SPLIT>(p, q.pa, q.pb, lg, rb_a, rb_b);
     const bool try_fast = p.f16_ok && p.win_vec;
     WinRound w0;
-#if MSW_EARLY_WIN_LOADS
     if (try_fast) load_round<SPLIT>(p, q, 0, lg, G, w0);
-#endif
     const int skew = SPLIT ? 2 * (G - 1) + 1 : G - 1;
     // wavefront steps, rounded up to a multiple of the steps per iteration
     // (the explicitly scheduled f16 loops of the pairs layout run four steps
@@ -714,9 +649,6 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     constexpr int kUnroll = (!SPLIT && explicit_sched(AFFINE, COORDS)) ? 4 : step_unroll(AFFINE, COORDS);
     const int steps = (wave_max_nonneg(max(q.na, q.nb)) + skew + kUnroll - 1) & ~(kUnroll - 1);
     uint32_t* stream = lds + g * p.lds_stride;
-#if !MSW_EARLY_WIN_LOADS
-    if (try_fast) load_round<SPLIT>(p, q, 0, lg, G, w0);
-#endif
     uint32_t rc[KR];
     read_codes<KR, SPLIT>(p, q, lg, rb_a, rb_b, rc);
     bool fast;
@@ -979,7 +911,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
         // One wavefront step: consumes t1 (this step's diagonal terms), produces
         // t1n (the next step's) from w, the window word of step t + 1.  Called
         // with alternating buffers so the hand-over needs no register copies.
-        uint32_t hpend = 0u;  // MSW_FOLD_PAIR: last row's H of the even step, folded with the odd one's
+        uint32_t hpend = 0u;  // last row's H of the even step, folded with the odd one's
         auto step = [&](int t, uint32_t w, const uint32_t (&t1)[KR], uint32_t (&t1n)[KR], auto parity)
                         __attribute__((always_inline)) {
             constexpr int kParity = decltype(parity)::value;
@@ -1057,13 +989,9 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
                 } else {
                     if (r & 1) {
                         best = track_max3(best, hprev, h);
-                    } else if (r + 1 == KR) {
-                        if constexpr (MSW_FOLD_PAIR) {
-                            if constexpr (kParity == 0) hpend = h;
-                            else best = track_max3(best, hpend, h);
-                        } else {
-                            best = F16 ? hmax(best, h) : pk_max(best, h);
-                        }
+                    } else if (r + 1 == KR) {  // an odd KR's last row: folded two steps at a time
+                        if constexpr (kParity == 0) hpend = h;
+                        else best = track_max3(best, hpend, h);
                     }
                     hprev = h;
                 }
@@ -1167,9 +1095,6 @@ __device__ __forceinline__ void trace_end(const SwParams& p, const WaveClock& w,
 // stay heaviest first.  Speed only (traffic), never correctness.
 template <uint32_t G>
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
-#ifdef MSW_NO_XCD_REMAP  // A/B builds (tools/build_variant.sh)
-    return b;
-#endif
     constexpr uint32_t span = 8u * G;
     const uint32_t base = b - b % span;
     if (base + span > nb) return b;

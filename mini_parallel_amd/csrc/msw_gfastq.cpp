@@ -33,6 +33,7 @@
 #include <vector>
 
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "../../include/msw.h"
@@ -518,14 +519,6 @@ int to_copied(msw_gfastq* g) {
     return fill_compressed(g, g->hc_cap);
 }
 
-uint64_t first_span_bytes() {
-    static const uint64_t v = [] {
-        const char* e = getenv("MSW_GFASTQ_FIRST_SPAN_MB");
-        return (e && atoll(e) > 0 ? (uint64_t)atoll(e) : 0ull) << 20;
-    }();
-    return v;
-}
-
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -540,17 +533,25 @@ int next_span(msw_gfastq* g) {
     if (g->mapped && g->reg_failed && (rc = to_copied(g))) return rc;
     if (g->mapped && !g->reg_len && g->map_off < g->fsize) register_window(g);  // no read-ahead ran
     if (g->mapped && g->reg_failed && (rc = to_copied(g))) return rc;
+    // A lane file must not change while it is read (the mapping is
+    // MAP_SHARED: touching pages past a truncation raises SIGBUS).  Checked
+    // before the host parses this span's member headers, so a file truncated
+    // between spans is an error instead of a signal.
+    if (g->mapped) {
+        struct stat sb;
+        if (fstat(fileno(g->f), &sb) != 0 || (uint64_t)sb.st_size < g->fsize)
+            return set_error(MSW_E_INVALID, "Error reading %s: the file shrank while it was being read",
+                             g->path.c_str());
+    }
     // 1. whole members whose output fits the span (compressed <= span bytes + 1 MiB)
     g->mem.clear();
     size_t used = 0;
     uint64_t obytes = 0;
-    // MSW_GFASTQ_FIRST_SPAN_MB: a shorter first span for the reader (scoring
-    // starts sooner).  Measured slower, off by default: 256 MB first spans
-    // 99-102 vs 104-105 M reads/s over 16 files, 67-69 vs 76 M over 2 files
-    // (profiles/r03/e2e/first_span_ab.jsonl) -- fewer members per inflate
-    // launch cost more than the earlier start wins.
-    const uint64_t cap = g->spans == 0 && first_span_bytes() ? std::min<uint64_t>(g->span, first_span_bytes())
-                                                              : g->span;
+    // Every span is full size: a shorter first span (scoring starts sooner)
+    // measured slower -- 256 MB first spans 99-102 vs 104-105 M reads/s over
+    // 16 files, 67-69 vs 76 M over 2 files (profiles/r03/e2e/first_span_ab.jsonl):
+    // fewer members per inflate launch cost more than the earlier start wins.
+    const uint64_t cap = g->span;
     for (;;) {
         if ((rc = index_members(g->hc, g->hc_len, kCarry, cap, g->in_cap, g->mem, &used, &obytes))) return rc;
         const bool full = obytes + 65536 > cap || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
@@ -608,6 +609,8 @@ int next_span(msw_gfastq* g) {
     GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
     GZ_TRY(hipStreamSynchronize(s));
     const double t_a = trace ? now_ms() : 0.0;
+    if (lead)  // uploads done: the member table holds offsets into hc again
+        for (msw::GzMember& m : g->mem) m.coff -= lead;
     if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
     // the upload of hc has completed: drop the consumed bytes and read ahead
     if (g->mapped) {

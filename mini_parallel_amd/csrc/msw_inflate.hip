@@ -1035,41 +1035,10 @@ __global__ __launch_bounds__(256) void gz_crc_kernel(const uint8_t* __restrict__
 hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint32_t n, uint8_t* out,
                              uint32_t* status, uint32_t* any_error, hipStream_t stream, uint32_t* prof) {
     if (n == 0) return hipSuccess;
-    // MSW_GZ_RING_KB: the output ring in LDS (tools/inflate_bench.py sweeps it)
-    static const int ring_kb = [] {
-        const char* e = getenv("MSW_GZ_RING_KB");
-        return e ? atoi(e) : kDefaultRingKb;
-    }();
-    // MSW_GZ_LDS_PAD: extra (dynamic) LDS bytes per wave, which caps the
-    // inflate waves per CU and leaves registers for kernels sharing the GPU
-    static const uint32_t lds_pad = [] {
-        const char* e = getenv("MSW_GZ_LDS_PAD");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    // MSW_GZ_WAVES_PER_SIMD: a grid of that many inflate waves per SIMD, each
-    // looping over members, so the rest of every CU (registers, LDS) stays
-    // free for the scoring kernel running beside it (0 = one block per member)
-    static const uint32_t waves_per_simd = [] {
-        const char* e = getenv("MSW_GZ_WAVES_PER_SIMD");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    static const uint32_t simds = [] {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return 4u * (uint32_t)cus;
-    }();
-    const uint32_t grid = waves_per_simd ? std::min<uint32_t>(n, waves_per_simd * simds) : n;
-#define GZ_LAUNCH(R) hipLaunchKernelGGL(gz_inflate_kernel<R>, dim3(grid), dim3(64), lds_pad, stream, cdata, members, n, \
-                                         out, status, any_error, prof)
-    switch (ring_kb) {
-        case 1: GZ_LAUNCH(1024); break;
-        case 2: GZ_LAUNCH(2048); break;
-        case 4: GZ_LAUNCH(4096); break;
-        case 16: GZ_LAUNCH(16384); break;
-        case 32: GZ_LAUNCH(32768); break;
-        default: GZ_LAUNCH(8192); break;
-    }
-#undef GZ_LAUNCH
+    // One wave per member; the 2 KiB output ring in LDS (kDefaultRingKb:
+    // 1 KiB measured the same, 4 / 8 KiB slower -- DESIGN.md 4.7).
+    hipLaunchKernelGGL(gz_inflate_kernel<kDefaultRingKb * 1024>, dim3(n), dim3(64), 0, stream, cdata, members, n,
+                       out, status, any_error, prof);
     return hipGetLastError();
 }
 

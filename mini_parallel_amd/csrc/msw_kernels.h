@@ -112,17 +112,7 @@ inline uint32_t vec_ok(const void* base, uint64_t stride) {
 }
 
 // Dynamic LDS bytes for one 64-lane block (one window stream per group).
-// MSW_SW_LDS_MIN (experiments): a floor on it, which caps the scoring
-// kernels' blocks per CU so another kernel (the GPU inflate) keeps room on
-// the same CUs.
-inline size_t lds_bytes(uint32_t lds_stride, uint32_t groups) {
-    static const size_t floor_bytes = [] {
-        const char* e = getenv("MSW_SW_LDS_MIN");
-        return e ? (size_t)strtoul(e, nullptr, 10) : (size_t)0;
-    }();
-    const size_t b = (size_t)groups * lds_stride * sizeof(uint32_t);
-    return b > floor_bytes ? b : floor_bytes;
-}
+inline size_t lds_bytes(uint32_t lds_stride, uint32_t groups) { return (size_t)groups * lds_stride * sizeof(uint32_t); }
 
 enum class Layout { kPairs, kSplit, kMixed };
 

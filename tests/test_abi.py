@@ -40,6 +40,23 @@ def test_library_exports_every_symbol():
         assert getattr(L, name) is not None
 
 
+def test_lib_path_override(tmp_path):
+    """MSW_LIB_PATH (A/B tooling) loads the named build instead of the
+    in-tree one; without it the in-tree library loads."""
+    import shutil
+    import sys
+    alt = tmp_path / "libmsw_alt.so"
+    shutil.copy(_lib.LIB_PATH, alt)
+    code = ("import sys; sys.path.insert(0, sys.argv[1]); from mini_parallel_amd import _lib; L = _lib.lib(); "
+            "print(_lib.LIB_PATH); print(L._name)")
+    env = dict(os.environ, MSW_LIB_PATH=str(alt))
+    out = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == [str(alt), str(alt)]
+    env.pop("MSW_LIB_PATH")
+    out = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split()[0] == os.path.join(ROOT, "mini_parallel_amd", "libmsw.so")
+
+
 def test_library_targets_gfx950():
     """The fat binary embeds a gfx950 code object (and nothing else)."""
     data = open(_lib.LIB_PATH, "rb").read()

@@ -269,10 +269,15 @@ def test_full_wgs_file_shards(tmp_path, oracle):
         rec = json.load(open(tmp_path / f"rec{r}.json"))
         assert rec["cpu_cores_used"] == rec["host_cpus_usable"] >= 1
         ck = json.load(open(tmp_path / f"checkpoint_{rec['run_id']}.json"))
+        names = [os.path.basename(x) for x in ds["files"]]
         for f in ck["files"]:
             name = os.path.basename(f["file_path"])
             assert name not in got
             got[name] = f["score"]
+            # messages and the checkpoint keep the file's place in the whole lane set
+            assert f["file_index"] == names.index(name) and f["file_index"] % 2 == r
+            assert f"Processing file {f['file_index'] + 1}/6: " in res.stdout
+            assert f"File {f['file_index'] + 1} done: " in res.stdout
     assert got == want
     env["WGS_FILE_SHARD"] = "2/2"
     res = run(["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"]], env=env, cwd=tmp_path)

@@ -157,6 +157,21 @@ def test_bgzf_lane_file(tmp_path, monkeypatch, no_libdeflate, crlf):
     assert list(pos) == [i * 7 for i in range(3000)]
 
 
+@pytest.mark.parametrize("threads", ["2", "5"])
+def test_bgzf_inflate_threads(tmp_path, monkeypatch, threads):
+    """MSW_INFLATE_THREADS (the CLI sets it when a file has several host CPUs):
+    a file's BGZF blocks inflated by several threads give the same chunks."""
+    from mini_parallel_amd.synthetic import bgzf_compress
+    monkeypatch.setenv("MSW_INFLATE_THREADS", threads)
+    rng = np.random.default_rng(11)
+    data = synth_fastq(5000, rng)
+    p = str(tmp_path / "t.fastq.gz")
+    open(p, "wb").write(bgzf_compress(data, block=4096))
+    got = []
+    process_fastq_file_in_chunks(p, 777, got.append)
+    assert got == reference_chunks(data, 777)
+
+
 def test_bgzf_corrupt_block_is_an_error(tmp_path):
     from mini_parallel_amd.synthetic import bgzf_compress
     rng = np.random.default_rng(10)

@@ -73,11 +73,7 @@ def main():
                    WGS_RUN_ID=f"e2e_{kind}_{readers}_v{vi}_{int(time.time() * 1000)}")
         if args.read_len > 256:
             env["MSW_MAX_READ_LEN"] = str(args.read_len + 16)  # room for the synthetic indels
-        if kind == "threads":
-            env["MSW_HOST_THREADS"] = str(readers)
-            env.pop("MSW_READERS", None)
-        else:
-            env["MSW_READERS"] = str(readers)
+        env["MSW_HOST_THREADS"] = str(readers)  # reader threads = host threads (capped at the file count)
         for kv in filter(None, extra_env.split(",")):
             k, v = kv.split("=", 1)
             env[k] = v
