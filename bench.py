@@ -621,6 +621,8 @@ def leg_pairs(job, ctx, cfg, args):
         par["mismatches"] += cpar["mismatches"]
     kernel_gcups = batch.cells / kern / 1e9
     alg = alg_bytes_of(batch, scoring)
+    # counter traffic of this leg's kernel at this size (tools/profile_round.sh)
+    tr = load_pmc_traffic(f"config{cfg}:{kind}") if (job.gpu and per_gpu == DEFAULT_PAIRS[cfg]) else None
     return {"workload": f"config{cfg}: {per_gpu} pairs/GPU of one global {n_total}-pair batch, reads "
                         f"{int(batch.read_len.min())}-{int(batch.read_len.max())} bp x windows "
                         f"{int(batch.win_len.min())}-{int(batch.win_len.max())} bp, {kind.replace('_', '+')}, "
@@ -631,7 +633,10 @@ def leg_pairs(job, ctx, cfg, args):
             "max_avg_launch_ms": round(kern_max * 1e3, 4), "launches": reps,
             "valu": valu_block(kind, kernel_gcups),
             "roofline_hbm": {"achieved": round(alg / kern / 1e9, 2), "frac": round(alg / kern / 1e9 / HBM_PEAK_GBPS, 5),
-                             "alg_bytes_per_launch": alg},
+                             "alg_bytes_per_launch": alg,
+                             "traffic": round(tr["hbm_bytes_per_launch"]) if tr else None,
+                             "traffic_over_alg": round(tr["hbm_bytes_per_launch"] / alg, 3) if tr else None,
+                             "traffic_detail": tr},
             "parity": par, "gathered_pairs": int(g[0].size), "host_to_host": h2h, "cpu_baseline": cpu,
             "gen_seconds": round(gen_s, 1)}
 
@@ -1419,6 +1424,7 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": round(traffic["hbm_bytes_per_launch"]) if traffic else None,
+                         "traffic_over_alg": round(traffic["hbm_bytes_per_launch"] / alg_bytes, 3) if traffic else None,
                          "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/pmc_traffic.json)",
                          "traffic_detail": traffic, "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4)},

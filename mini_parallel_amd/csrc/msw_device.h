@@ -134,6 +134,12 @@ struct PairMeta {
 #ifndef MSW_PROBE_NO_READ
 #define MSW_PROBE_NO_READ 0
 #endif
+// -DMSW_PROBE_CONST_LEN=1: the pair lengths are the config-2 constants (150 /
+// 300) instead of loads, so with the two probes above FETCH_SIZE is what the
+// launch fetches besides the sequence bytes and the lengths (code, arguments).
+#ifndef MSW_PROBE_CONST_LEN
+#define MSW_PROBE_CONST_LEN 0
+#endif
 
 template <bool SPLIT>
 __device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t block, bool active) {
@@ -161,6 +167,9 @@ __device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t
         na = (int)(la >> 16);
         mb = (int)(lb & 0xFFFFu);
         nb = (int)(lb >> 16);
+    } else if (MSW_PROBE_CONST_LEN) {
+        ma = mb = 150;
+        na = nb = 300;
     } else {
         ma = p.read_len[q.pa];
         na = p.win_len[q.pa];

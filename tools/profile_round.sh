@@ -9,6 +9,9 @@ set -euo pipefail
 R=${1:-r01}
 OUT=gpurun_out/prof_$R
 mkdir -p "$OUT"
+# the commit of the profiled tree (the GPU box has no .git: pass it in)
+echo "${MSW_COMMIT:-unknown}" > "$OUT/COMMIT"
+export TMPDIR=/tmp
 for CFG in 2 3 5; do
   case $CFG in
     2) ARGS="--steps 50 --warmup 5" ;;

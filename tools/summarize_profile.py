@@ -30,6 +30,14 @@ def main():
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
     summary, traffic = {}, {}
+    # the commit whose build was profiled: gpurun_out/prof_<round>/COMMIT (written by
+    # tools/profile_round.sh from the tree it ran), else this checkout's HEAD
+    try:
+        commit = open(os.path.join(src, "COMMIT")).read().strip()
+    except OSError:
+        import subprocess
+        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                text=True).stdout.strip()
     for cfg in (2, 3, 5):
         d = os.path.join(src, f"c{cfg}")
         if not os.path.isdir(d):
@@ -43,15 +51,16 @@ def main():
         for k in sorted({k for k, _ in c}):
             per_kernel[k] = {cn: v for (kn, cn), v in c.items() if kn == k}
         summary[f"config{cfg}"] = per_kernel
-        # the dominant (scoring) kernel of the config
-        main_k = [k for k in per_kernel if "cut_windows" not in k]
+        # the dominant (scoring) kernel of the config: the one fetching most
+        main_k = sorted((k for k in per_kernel if "FETCH_SIZE" in per_kernel[k] and "WRITE_SIZE" in per_kernel[k]),
+                        key=lambda k: -per_kernel[k]["FETCH_SIZE"])[:1]
         for k in main_k:
             m = per_kernel[k]
-            if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            if True:
                 fetch_b, write_b = m["FETCH_SIZE"] * 1024, m["WRITE_SIZE"] * 1024
                 traffic[f"config{cfg}:{KIND[cfg]}"] = {
                     "kernel": k, "fetch_bytes_raw": fetch_b, "write_bytes": write_b,
-                    "hbm_bytes_per_launch": fetch_b * 2 + write_b,
+                    "hbm_bytes_per_launch": fetch_b * 2 + write_b, "round": rnd, "commit": commit,
                     "note": "FETCH_SIZE x 2 (gfx950 reports half of wide 16 B/lane reads, "
                             "MI355X_MICROARCH.md HBM section) + WRITE_SIZE; per launch; the batch is "
                             "re-read every step and may be served from the 256 MiB Infinity Cache"}
