@@ -27,12 +27,12 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402  (the bench's dataset builder and constants)
 
 
-def run_cli(d, files, gpu_inflate, tag, out_dir):
+def run_cli(d, files, gpu_inflate, tag, out_dir, cli=None):
     rec_path = os.path.join(out_dir, f"rec_{tag}.json")
     env = dict(os.environ, WGS_DATA_DIR=d, WGS_SAMPLE_ID="SYN", WGS_LANES=str(bench.C4_LANES),
                WGS_READS_PER_LANE=str(bench.C4_READS_PER_LANE), GPU_CHUNK_SIZE_READS="65536",
                MSW_GPU_INFLATE=gpu_inflate, WGS_RUN_ID=f"c4full_{tag}_{os.getpid()}")
-    cmd = [os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini"), "--full-wgs", "--gpu", "--score-mode", "sw",
+    cmd = [cli or os.path.join(ROOT, "mini_parallel_amd", "rustseq_mini"), "--full-wgs", "--gpu", "--score-mode", "sw",
            "--reference", os.path.join(d, "reference.fa"), "--window", str(bench.C4_WINDOW),
            "--checkpoint-dir", "/tmp", "--json", rec_path]
     t0 = time.perf_counter()
