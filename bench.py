@@ -84,6 +84,8 @@ I32_OPS_PER_CELL = {"linear": 6, "linear_coords": 8, "affine": 11, "affine_coord
 # SIMD, config 2: 1000 waves on 1024 SIMDs) at best every 4.75 cycles.
 PACKED_ISSUE_CYCLES, LONE_WAVE_ISSUE_CYCLES = 4.1, 4.75
 
+PREHEAT_S = 0.1  # seconds of back-to-back steps before each timed region (Job.preheat)
+
 # config-4 leg: 8 lanes x R1/R2 BGZF lane files (aligner.rs:198-204 naming) of
 # 25 M reads = 400 M reads (BASELINE config 4: "8 lanes x ~50 M reads"), each
 # file 25 segments of 1 M reads from a pool of 32 distinct pre-scored segments
@@ -524,10 +526,11 @@ class Job:
 
     def fence(self):
         """Start of a timed region (and a plain rendezvous): synchronize,
-        barrier, synchronize."""
+        barrier, synchronize.  One rank has no one to wait for: no barrier
+        (the gathers and reductions still run through the group)."""
         from mini_parallel_amd import dist as mdist
         self.sync()
-        if mdist.active():
+        if mdist.active() and self.world > 1:
             import torch.distributed as dist
             dist.barrier()
         self.sync()
@@ -540,6 +543,23 @@ class Job:
         t = time.perf_counter()
         self.fence()
         return t
+
+    def preheat(self, step, seconds=PREHEAT_S):
+        """After the warm-up steps: repeat the step back to back until the GPU
+        has run it for `seconds`.  An idle GPU drops its clock and takes ~10 ms
+        of load to ramp back (config 2: 49.4 us per launch after a 10 ms idle
+        spell, 44.8 after ~200 launches; tools/launch_series.py), so a 1 ms
+        timed region right after setup measures the ramp, not the kernel.
+        Untimed; reported as `preheat` beside `warmup`."""
+        if not self.gpu or seconds <= 0:
+            return {"steps": 0, "seconds": 0.0}
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            for _ in range(20):
+                step()
+            n += 20
+            self.sync()
+        return {"steps": n, "seconds": round(time.perf_counter() - t0, 3)}
 
     def max(self, vals):
         from mini_parallel_amd import dist as mdist
@@ -580,6 +600,7 @@ def leg_pairs(job, ctx, cfg, args):
         w = GpuWorkload(ctx, job.dev, job.stream, cfg, batch, scoring)
         for _ in range(2):
             w.step()
+        job.preheat(w.step)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         job.fence()
         t0 = time.perf_counter()
@@ -650,7 +671,7 @@ def leg_pairs(job, ctx, cfg, args):
             "gen_seconds": round(gen_s, 1)}
 
 
-def pipelined_steps(job, ctx, cfg, batch, scoring, work, args):
+def pipelined_steps(job, ctx, cfg, batch, scoring, work, s2, args):
     """"pipelined_two_streams": the same K steps over the same batch, issued
     alternately on two streams (a second score buffer on a second stream),
     so step k + 1's waves start while step k's drain -- two waves per SIMD
@@ -658,11 +679,11 @@ def pipelined_steps(job, ctx, cfg, batch, scoring, work, args):
     still one complete pass over the batch; the serial one-stream rate stays
     `value`.  Scores of both buffers must equal."""
     import torch
-    s2 = torch.cuda.Stream(job.dev)
     w2 = GpuWorkload(ctx, job.dev, s2, cfg, batch, scoring)
     pair = (work.step, w2.step)
     for k in range(max(2, args.warmup)):
         pair[k & 1]()
+    job.preheat(lambda: (pair[0](), pair[1]()))
     job.fence()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -1344,8 +1365,11 @@ def main(argv=None):
         dev = torch.device("cuda", local_rank)
         from mini_parallel_amd import Context
         ctx = Context(local_rank)
-        # A dedicated (non-null) stream: the kernels and the timing events share it.
+        # A dedicated (non-null) stream: the kernels and the timing events share
+        # it; a second one, created beside it (HIP maps streams onto its
+        # hardware queues as they are created), for pipelined_steps.
         stream = torch.cuda.Stream(dev)
+        stream2 = torch.cuda.Stream(dev)
         torch.cuda.set_stream(stream)
         work = GpuWorkload(ctx, dev, stream, cfg, batch, scoring)
         step = work.step
@@ -1359,6 +1383,7 @@ def main(argv=None):
 
     for _ in range(args.warmup):
         step()
+    preheat = job.preheat(step)
     job.fence()
 
     if gpu:
@@ -1386,7 +1411,7 @@ def main(argv=None):
         (g_score,) = mdist.gather_results(torch.from_numpy(holder["s"]))
         g_i = g_j = None
 
-    pipe = pipelined_steps(job, ctx, cfg, batch, scoring, work, args) if gpu else None
+    pipe = pipelined_steps(job, ctx, cfg, batch, scoring, work, stream2, args) if gpu else None
 
     # The other BASELINE configs, on every rank (each leg fences and gathers).
     extra = {}
@@ -1475,6 +1500,9 @@ def main(argv=None):
             "pcie_inclusive": pcie,
             "cut_windows_roofline": cut,
             "pipelined_two_streams": pipe,
+            "preheat": dict(preheat, note="untimed repeats of the step after the warm-up until the GPU has "
+                                          "run it back to back for the time stated: the clock ramps over ~10 ms "
+                                          "of load (tools/launch_series.py, DESIGN.md 5)"),
             "gathered_scores": gathered,
             "collectives": {"backend": mdist.backend(), "world": world, "calls_rank0": dict(mdist.CALLS),
                             "note": "every max / sum / gather / barrier of the run goes through this process "
