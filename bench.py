@@ -1300,6 +1300,22 @@ def leg_config3_fastq(job, args):
             "dataset": {k: v for k, v in (args._c3f_meta or {}).items() if not k.startswith("_")}}
 
 
+class _stdout_to_stderr:
+    """File descriptor 1 pointed at 2 for the block (native libraries print
+    on fd 1 directly, below sys.stdout)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def _torch():
     import torch
     return torch
@@ -1348,6 +1364,12 @@ def main(argv=None):
     pg_init = "env://" if "WORLD_SIZE" in os.environ else f"tcp://127.0.0.1:{_free_port()}"
     dist.init_process_group("nccl" if gpu else "gloo", init_method=pg_init, rank=rank, world_size=world,
                             timeout=datetime.timedelta(minutes=30))
+    # Build the communicator now, not inside a leg, and keep RCCL's version
+    # banner (printed on stdout at communicator creation) off the one-line
+    # stdout contract.
+    with _stdout_to_stderr():
+        from mini_parallel_amd import dist as _md
+        _md.sum_over_ranks([0], device=torch.device("cuda", local_rank) if gpu else None)
     from mini_parallel_amd import dist as mdist
     from mini_parallel_amd.synthetic import config_shard
 
@@ -1403,6 +1425,11 @@ def main(argv=None):
     # every rank scores its own shard: the job's cells and ranks are sums over ranks
     job_cells, ranks_ran = job.sum([cells, 1])
 
+    # Two batches in flight (an extra figure, not `value`).  Before any
+    # all_gather: after one, kernels on the two streams stopped overlapping on
+    # the box (tools/pipe_probe.py: 34.7 -> 42.7 us per step).
+    pipe = pipelined_steps(job, ctx, cfg, batch, scoring, work, stream2, args) if gpu else None
+
     # Final score/coordinate gather over RCCL (outside the timed region): the
     # only collective of the path.  Concatenated in rank order = global order.
     if gpu:
@@ -1410,8 +1437,6 @@ def main(argv=None):
     else:
         (g_score,) = mdist.gather_results(torch.from_numpy(holder["s"]))
         g_i = g_j = None
-
-    pipe = pipelined_steps(job, ctx, cfg, batch, scoring, work, stream2, args) if gpu else None
 
     # The other BASELINE configs, on every rank (each leg fences and gathers).
     extra = {}
