@@ -852,19 +852,20 @@ def c4_layout(args):
 
 
 def _copy_into(dst, srcs, tail):
-    """dst = the concatenation of the files srcs, then the bytes tail
-    (copy_file_range: in-kernel copies, reflinks where the file system has them)."""
+    """dst = the concatenation of the files srcs, then the bytes tail.
+    Plain reads and writes, so the lane file's own pages are in the page
+    cache, as a lane set that was just written or read is: copy_file_range
+    reflinked the segments on the box's file system, which left every run
+    paging the lane files in from disk (the first window of each file
+    ~150 ms, GPU idle; tools/c4_trace.sh)."""
     with open(dst, "wb") as fo:
         for s in srcs:
             with open(s, "rb") as fi:
-                left = os.fstat(fi.fileno()).st_size
-                off = 0
-                while left > 0:
-                    k = os.copy_file_range(fi.fileno(), fo.fileno(), min(left, 1 << 30), off)
-                    if k <= 0:
-                        raise OSError(f"copy_file_range stalled copying {s}")
-                    off += k
-                    left -= k
+                while True:
+                    buf = fi.read(64 << 20)
+                    if not buf:
+                        break
+                    fo.write(buf)
         fo.write(tail)
         return fo.tell()
 
