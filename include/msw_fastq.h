@@ -103,6 +103,15 @@ int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out);
  * two slabs alternate), so scoring enqueued on the previous file's last
  * batches may still be running while the new file is inflated and parsed. */
 int msw_gfastq_reset(msw_gfastq* g, const char* path);
+/* Name the lane file the next msw_gfastq_reset will open: it is opened,
+ * mapped and its first window of compressed bytes pinned by a host thread
+ * now, beside the current file's spans, so the reset adopts it instead of
+ * waiting for it (a new file's first window cost ~18-25 ms against 2-4 ms
+ * for later ones: tools/gfastq_trace_c4.sh).  Optional; a reset to another
+ * path opens that path as usual, and failures here only leave the reset to
+ * do the work.  The --full-wgs driver's per-file loop (aligner.rs:246-339)
+ * prefetches the file it will take next. */
+int msw_gfastq_prefetch(msw_gfastq* g, const char* path);
 /* lines (valid), reads, errors (invalid lines), bases, compressed and inflated bytes so far (this file) */
 void msw_gfastq_stats(const msw_gfastq* g, uint64_t* lines, uint64_t* reads, uint64_t* errors, uint64_t* bases,
                       uint64_t* bytes_in, uint64_t* bytes_out);

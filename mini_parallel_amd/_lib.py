@@ -35,7 +35,7 @@ EXPORTED = (
 FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_next_packed",
                   "msw_fastq_stats", "msw_fastq_count_bases", "msw_is_bgzf", "msw_gfastq_open",
                   "msw_gfastq_next", "msw_gfastq_stats", "msw_gfastq_close", "msw_bgzf_inflate",
-                  "msw_gfastq_reset")
+                  "msw_gfastq_reset", "msw_gfastq_prefetch")
 
 
 class MswError(RuntimeError):
@@ -152,6 +152,7 @@ def _declare(L):
         "msw_gfastq_stats": (None, [P] + [ctypes.POINTER(ctypes.c_uint64)] * 6),
         "msw_gfastq_close": (None, [P]),
         "msw_gfastq_reset": (I, [P, ctypes.c_char_p]),
+        "msw_gfastq_prefetch": (I, [P, ctypes.c_char_p]),
         "msw_bgzf_inflate": (I, [P, P, ctypes.c_uint64, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     }
     for name, (res, args) in sigs.items():

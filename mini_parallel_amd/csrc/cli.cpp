@@ -802,12 +802,21 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     maybe_finish(fi);
                 };
                 // next file for this worker: reset the reader (its compressed
-                // bytes start loading in the background), false when none is left
+                // bytes start loading in the background), false when none is
+                // left.  The worker claims the file after it at the same time
+                // and has the reader pin that file's first window now
+                // (msw_gfastq_prefetch), so the next switch does not wait on it.
+                const size_t kNone = ~(size_t)0;
+                size_t pending = kNone;
+                auto claim = [&]() -> size_t {
+                    const size_t k = next_file.fetch_add(1);
+                    return k < todo.size() ? todo[k] : kNone;
+                };
                 auto open_next = [&](size_t* fi_out) -> bool {
                     for (;;) {
-                        const size_t k = next_file.fetch_add(1);
-                        if (k >= todo.size()) return false;
-                        const size_t fi = todo[k];
+                        const size_t fi = pending != kNone ? pending : claim();
+                        pending = kNone;
+                        if (fi == kNone) return false;
                         FileState& f = *st[fi];
                         f.t0 = Clock::now();
                         open_files[fi] = {0, false};
@@ -829,6 +838,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                             reader_done(fi);
                             continue;
                         }
+                        pending = claim();
+                        if (pending != kNone) (void)msw_gfastq_prefetch(gr, st[pending]->path.c_str());
                         *fi_out = fi;
                         return true;
                     }

@@ -300,6 +300,17 @@ struct msw_gfastq {
     uint64_t map_off = 0;              // first byte not yet inflated
     uint64_t reg_lo = 0, reg_len = 0;  // the registered window
     bool reg_failed = false;
+    // msw_gfastq_prefetch: the next lane file opened, mapped and its first
+    // window pinned by a host thread while this file's spans run; open_file
+    // adopts it when the caller resets to that path
+    struct Prefetch {
+        std::string path;
+        FILE* f = nullptr;
+        uint64_t fsize = 0, reg_len = 0;
+        uint8_t* map = nullptr;
+        bool ok = false;
+        std::thread th;
+    } pf;
     // read-ahead: while the GPU inflates / the caller scores, a host thread
     // reads the next span's compressed bytes into hc after hc_len
     std::thread filler;
@@ -352,10 +363,29 @@ void join_filler(msw_gfastq* g) {
     if (g->filler.joinable()) g->filler.join();
 }
 
+// Drop a prefetched file that was not adopted (or join it before adopting).
+void join_prefetch(msw_gfastq* g) {
+    if (g->pf.th.joinable()) g->pf.th.join();
+}
+
+void drop_prefetch(msw_gfastq* g) {
+    join_prefetch(g);
+    msw_gfastq::Prefetch& p = g->pf;
+    if (p.reg_len) (void)hipHostUnregister(p.map);
+    if (p.map) munmap(p.map, (size_t)p.fsize);
+    if (p.f) fclose(p.f);
+    p.f = nullptr;
+    p.map = nullptr;
+    p.fsize = p.reg_len = 0;
+    p.ok = false;
+    p.path.clear();
+}
+
 void unmap_file(msw_gfastq* g);
 
 void release(msw_gfastq* g) {
     join_filler(g);
+    drop_prefetch(g);
     (void)hipSetDevice(g->device);
     if (g->rs) (void)hipStreamSynchronize(g->rs);
     unmap_file(g);
@@ -686,6 +716,7 @@ int next_span(msw_gfastq* g) {
 // buffers kept.  The parse state goes back to line 0 on the reader stream.
 int open_file(msw_gfastq* g, const char* path) {
     join_filler(g);
+    join_prefetch(g);
     if (g->mapped || g->map) {
         // the previous file's last window may still be uploading
         GZ_TRY(hipSetDevice(g->device));
@@ -709,6 +740,31 @@ int open_file(msw_gfastq* g, const char* path) {
     g->fill_rc = 0;
     g->last_used = 0;
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
+    if (g->pf.ok && g->pf.path == path) {
+        // prefetched (msw_gfastq_prefetch): file open, mapped, first window
+        // [0, reg_len) pinned -- the state register_window leaves behind
+        msw_gfastq::Prefetch& p = g->pf;
+        g->f = p.f;
+        g->fsize = p.fsize;
+        g->map = p.map;
+        g->mapped = true;
+        g->map_off = g->reg_lo = 0;
+        g->reg_len = p.reg_len;
+        g->hc = g->map;
+        g->hc_len = g->hc_cap = (size_t)p.reg_len;
+        g->fread_off = p.reg_len;
+        p.f = nullptr;
+        p.map = nullptr;
+        p.fsize = p.reg_len = 0;
+        p.ok = false;
+        p.path.clear();
+        if (g->d_state) {
+            GZ_TRY(hipSetDevice(g->device));
+            GZ_TRY(hipMemcpyAsync(g->d_state, g->d_state0, sizeof(msw::ParseState), hipMemcpyDeviceToDevice, g->rs));
+        }
+        return MSW_OK;
+    }
+    drop_prefetch(g);  // prefetched another path: not needed
     g->f = fopen(path, "rb");
     if (!g->f) return set_error(MSW_E_INVALID, "Failed to open file %s", path);
     fseeko(g->f, 0, SEEK_END);
@@ -833,6 +889,46 @@ int msw_gfastq_reset(msw_gfastq* g, const char* path) {
     const int rc = open_file(g, path);
     if (rc) g->failed = rc;
     return rc;
+}
+
+int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
+    if (!g || !path) return set_error(MSW_E_INVALID, "reader/path is NULL");
+    drop_prefetch(g);
+    const char* nm = getenv("MSW_GZ_NO_MAP");
+    if (nm && atoi(nm) != 0) return MSW_OK;  // copied mode: nothing to pin ahead
+    g->pf.path = path;
+    const size_t cap = g->in_cap;
+    const int device = g->device;
+    msw_gfastq::Prefetch* p = &g->pf;
+    try {
+        p->th = std::thread([p, cap, device]() {
+            // any failure leaves ok = false: reset then opens the file the usual way
+            p->f = fopen(p->path.c_str(), "rb");
+            if (!p->f) return;
+            if (fseeko(p->f, 0, SEEK_END) != 0) return;
+            p->fsize = (uint64_t)ftello(p->f);
+            fseeko(p->f, 0, SEEK_SET);
+            setvbuf(p->f, nullptr, _IONBF, 0);
+            uint8_t h[18];
+            if (p->fsize < 18 || fread(h, 1, 18, p->f) != 18 || member_size(h) < 26) return;
+            fseeko(p->f, 0, SEEK_SET);
+            void* m = mmap(nullptr, (size_t)p->fsize, PROT_READ, MAP_SHARED, fileno(p->f), 0);
+            if (m == MAP_FAILED) return;
+            p->map = (uint8_t*)m;
+            (void)madvise(m, (size_t)p->fsize, MADV_SEQUENTIAL);
+            const uint64_t hi = std::min<uint64_t>(p->fsize, cap);
+            if (hipSetDevice(device) != hipSuccess ||
+                hipHostRegister(p->map, (size_t)hi, hipHostRegisterReadOnly) != hipSuccess) {
+                (void)hipGetLastError();
+                return;
+            }
+            p->reg_len = hi;
+            p->ok = true;
+        });
+    } catch (const std::exception&) {
+        g->pf.path.clear();  // no thread to spare: reset opens it then
+    }
+    return MSW_OK;
 }
 
 int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {

@@ -119,6 +119,15 @@ class GpuFastqReader:
         except Exception:
             pass
 
+    def reset(self, path: str) -> None:
+        """msw_gfastq_reset: read another lane file with the same buffers."""
+        self.path = path
+        check(lib().msw_gfastq_reset(self._h, path.encode()))
+
+    def prefetch(self, path: str) -> None:
+        """msw_gfastq_prefetch: open the file the next reset() names ahead of time."""
+        check(lib().msw_gfastq_prefetch(self._h, path.encode()))
+
     def next_batch(self, host: bool = True):
         """-> DevReadsT, or with host=True (seqs u8[n, stride], lens u16[n][, pos i64[n]])."""
         d = DevReadsT()

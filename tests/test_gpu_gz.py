@@ -232,6 +232,46 @@ def test_reader_matches_host_reader(gpu_ctx, tmp_path, monkeypatch, block, crlf,
     assert n == 20_000
 
 
+def _drain(g):
+    seqs, lens, pos = [], [], []
+    while True:
+        s, ln, p = g.next_batch()
+        if len(ln) == 0:
+            break
+        seqs.append(s)
+        lens.append(ln)
+        pos.append(p)
+    return np.concatenate(seqs), np.concatenate(lens), np.concatenate(pos)
+
+
+@pytest.mark.parametrize("mode", ["map", "copy"])
+def test_reader_prefetch_next_file(gpu_ctx, tmp_path, monkeypatch, mode):
+    """msw_gfastq_prefetch: the next file opened and its first window pinned
+    while the current one is read; reset() to that path adopts it, reset() to
+    another path (or after prefetching a missing file) opens that path as
+    usual; every file reads exactly as the host reader reads it."""
+    monkeypatch.setenv("MSW_GZ_NO_MAP", "1" if mode == "copy" else "0")
+    files = []
+    for k in range(4):
+        p = tmp_path / f"lane{k}.fastq.gz"
+        p.write_bytes(bgzf_compress(fastq_text(6_000 + 500 * k, 40 + k), 6))
+        files.append(str(p))
+    with GpuFastqReader(gpu_ctx, files[0], 256, 2500, with_pos=True, span_bytes=1 << 20) as g:
+        g.prefetch(files[1])  # adopted by the next reset
+        got = [_drain(g)]
+        g.reset(files[1])
+        g.prefetch(files[3])  # not adopted: the reset names another file
+        got.append(_drain(g))
+        g.reset(files[2])
+        g.prefetch(str(tmp_path / "missing.fastq.gz"))  # fails in the background; harmless
+        got.append(_drain(g))
+        g.reset(files[3])
+        got.append(_drain(g))
+    for f, (gs, gl, gp) in zip(files, got):
+        hs, hl, hp, _ = host_reads(f)
+        assert np.array_equal(hl, gl) and np.array_equal(hp, gp) and np.array_equal(hs, gs), f
+
+
 @pytest.mark.parametrize("threads", ["3", "8"])
 def test_reader_parallel_compressed_reads(gpu_ctx, tmp_path, monkeypatch, threads):
     """Compressed top-ups split over several positioned-read threads
