@@ -140,7 +140,9 @@ def parse(argv=None):
                     help="config-4 leg: reads per pooled segment (lane files are made of segments)")
     ap.add_argument("--c4-pool", type=int, default=C4_POOL, help="config-4 leg: distinct segments in the pool")
     ap.add_argument("--c3-fastq-reads", type=int, default=1_000_000,
-                    help="config-3 FASTQ leg: reads over its 16 lane files (0 = skip the leg)")
+                    help="config-3 FASTQ leg: reads over its lane files (0 = skip the leg)")
+    ap.add_argument("--c3-fastq-lanes", type=int, default=8,
+                    help="config-3 FASTQ leg: lanes (R1 + R2 lane files each)")
     ap.add_argument("--c4-dir", default="/tmp/msw_bench_c4",
                     help="configs 3 / 4 FASTQ legs: where the lane files are generated (reused across runs)")
     ap.add_argument("--no-h2h", action="store_true", help="config-3 leg: skip the host-to-host rate")
@@ -930,7 +932,7 @@ def ensure_c4_dataset(args) -> dict:
 # config 3 from FASTQ (BASELINE: "1M synthetic 150 bp reads ... affine-gap
 # score + best-cell coord, async FASTQ chunk staging"): 16 lane files of
 # 62,500 reads, every read's (score, end_i, end_j) compared with the oracle.
-C3F_LANES, C3F_RPL, C3F_GENOME, C3F_SEED = 8, 2, 64 << 20, 1003
+C3F_RPL, C3F_GENOME, C3F_SEED = 2, 64 << 20, 1003
 
 
 def _c3_file_job(job):
@@ -956,10 +958,10 @@ def _c3_file_job(job):
 
 
 def c3f_layout(args):
-    n_files = C3F_LANES * C3F_RPL
+    n_files = args.c3_fastq_lanes * C3F_RPL
     per = args.c3_fastq_reads // n_files
-    d = os.path.join(args.c4_dir, f"c3fastq_{C3F_LANES}x{C3F_RPL}_r{per}_g{C3F_GENOME}_s{C3F_SEED}")
-    return d, [os.path.join(d, n) for n in _lane_names(C3F_LANES, C3F_RPL)], per
+    d = os.path.join(args.c4_dir, f"c3fastq_{args.c3_fastq_lanes}x{C3F_RPL}_r{per}_g{C3F_GENOME}_s{C3F_SEED}")
+    return d, [os.path.join(d, n) for n in _lane_names(args.c3_fastq_lanes, C3F_RPL)], per
 
 
 def ensure_c3f_dataset(args) -> dict:
@@ -1221,7 +1223,7 @@ def leg_config3_fastq(job, args):
     stats, err, cells, recs, idx = [0.0] * 5, "", 0, [], []
     setup = [0.0] * len(SETUP_PHASES)
     if job.gpu:
-        rec, ck, proc, wd, err = run_wgs_child(job, d, C3F_LANES, C3F_RPL, os.path.join(d, "reference.fa"),
+        rec, ck, proc, wd, err = run_wgs_child(job, d, args.c3_fastq_lanes, C3F_RPL, os.path.join(d, "reference.fa"),
                                                ["--gap-model", "affine", "--scores-out", "{wd}"], "c3f", 600)
         if not err:
             for fr in sorted(ck["files"], key=lambda x: files.index(x["file_path"])):
