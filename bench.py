@@ -140,9 +140,8 @@ def parse(argv=None):
                     help="config-4 leg: reads per pooled segment (lane files are made of segments)")
     ap.add_argument("--c4-pool", type=int, default=C4_POOL, help="config-4 leg: distinct segments in the pool")
     ap.add_argument("--c3-fastq-reads", type=int, default=1_000_000,
-                    help="config-3 FASTQ leg: reads over its lane files (0 = skip the leg)")
-    ap.add_argument("--c3-fastq-lanes", type=int, default=8,
-                    help="config-3 FASTQ leg: lanes (R1 + R2 lane files each)")
+                    help="config-3 FASTQ leg: reads per GPU, as one lane (R1 + R2 lane files) per GPU "
+                         "(0 = skip the leg)")
     ap.add_argument("--c4-dir", default="/tmp/msw_bench_c4",
                     help="configs 3 / 4 FASTQ legs: where the lane files are generated (reused across runs)")
     ap.add_argument("--no-h2h", action="store_true", help="config-3 leg: skip the host-to-host rate")
@@ -957,18 +956,26 @@ def _c3_file_job(job):
     return {"bytes": len(data), "cells": int(w.cells), "reads": int(n), "oracle_s": dt}
 
 
-def c3f_layout(args):
-    n_files = args.c3_fastq_lanes * C3F_RPL
-    per = args.c3_fastq_reads // n_files
-    d = os.path.join(args.c4_dir, f"c3fastq_{args.c3_fastq_lanes}x{C3F_RPL}_r{per}_g{C3F_GENOME}_s{C3F_SEED}")
-    return d, [os.path.join(d, n) for n in _lane_names(args.c3_fastq_lanes, C3F_RPL)], per
+def c3f_layout(args, world):
+    """N lanes x R1/R2 = 2N lane files for N GPUs, each GPU's reads split
+    over two files: rank r takes lane files r and r + N (WGS_FILE_SHARD), so
+    the leg is weak-scaled like the HBM-resident config-3 leg.  (One lane per GPU
+    rather than many small files: a file's first span cannot overlap its own
+    inflate with scoring, so 16 files of 62.5k reads ran at 20 M reads/s and
+    2 files of 500k at 40 M; smaller spans were slower still --
+    profiles/r04/e2e/c3f_layout.jsonl, c3f_span.jsonl.)"""
+    per = args.c3_fastq_reads // C3F_RPL
+    d = os.path.join(args.c4_dir, f"c3fastq_{world}x{C3F_RPL}_r{per}_g{C3F_GENOME}_s{C3F_SEED}")
+    # lane-major names (L001_R1, L001_R2, L002_R1, ...); rank r's files are r and r + N
+    names = _lane_names(world, C3F_RPL)
+    return d, [os.path.join(d, n) for n in names], per
 
 
-def ensure_c3f_dataset(args) -> dict:
+def ensure_c3f_dataset(args, world) -> dict:
     from mini_parallel_amd.synthetic import wgs_genome
     from oracle import oracle_lib
     global _POOL_GENOME
-    d, files, per = c3f_layout(args)
+    d, files, per = c3f_layout(args, world)
     names = [os.path.basename(p) for p in files]
     m = _marker_ok(d, names)
     if m is not None:
@@ -1218,12 +1225,12 @@ def leg_config3_fastq(job, args):
     (bad,) = job.sum([1 if (args._c3f_meta or {}).get("error") else 0])  # only rank 0 generated
     if bad:
         return None if job.rank else {"error": args._c3f_meta["error"], "parity": {"bit_exact": False}}
-    d, files, per = c3f_layout(args)
+    d, files, per = c3f_layout(args, job.world)
     F = len(files)
     stats, err, cells, recs, idx = [0.0] * 5, "", 0, [], []
     setup = [0.0] * len(SETUP_PHASES)
     if job.gpu:
-        rec, ck, proc, wd, err = run_wgs_child(job, d, args.c3_fastq_lanes, C3F_RPL, os.path.join(d, "reference.fa"),
+        rec, ck, proc, wd, err = run_wgs_child(job, d, job.world, C3F_RPL, os.path.join(d, "reference.fa"),
                                                ["--gap-model", "affine", "--scores-out", "{wd}"], "c3f", 600)
         if not err:
             for fr in sorted(ck["files"], key=lambda x: files.index(x["file_path"])):
@@ -1286,7 +1293,7 @@ def leg_config3_fastq(job, args):
     return {"workload": f"config3 from FASTQ: {F} BGZF lane files x {per} reads of 150 bp = {F * per} reads, "
                         f"{C3F_GENOME >> 20} Mbp HBM-resident genome, window {C4_WINDOW}, affine (open 3, extend 1) "
                         "+ best cell, per-read records (--scores-out)",
-            "n_ranks": job.world, "scaling": "strong", "reads": reads,
+            "n_ranks": job.world, "scaling": "weak", "reads": reads, "reads_per_gpu": args.c3_fastq_reads,
             "gcups_end_to_end": round(int(tot[0]) / (wall_ms * 1e6), 1),
             "gcups_incl_setup": round(int(tot[0]) / (setup_wall_ms * 1e6), 1),
             "reads_per_s": round(reads / (wall_ms * 1e-3)),
@@ -1338,7 +1345,7 @@ def main(argv=None):
         world = args.gpus or 1
         if world > 1:
             if args.cpu_standin or visible_gpus() >= world:
-                prepare_datasets(args, extras)  # before the ranks start (they reuse it)
+                prepare_datasets(args, extras, world)  # before the ranks start (they reuse it)
             return launch_ranks(args, argv)
     rank = int(os.environ.get("RANK", 0))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
@@ -1346,7 +1353,7 @@ def main(argv=None):
     args._c4_meta = args._c3f_meta = None
     if rank == 0:
         # before anything touches the GPU; the other ranks wait in init_process_group
-        prepare_datasets(args, extras)
+        prepare_datasets(args, extras, world)
 
     import datetime
 
@@ -1546,7 +1553,7 @@ def main(argv=None):
     return 0
 
 
-def prepare_datasets(args, extras):
+def prepare_datasets(args, extras, world):
     """The lane sets of the FASTQ legs (config 4, config 3 from FASTQ), written
     once before any rank touches a GPU.  A failure (e.g. no disk space) is
     kept as the leg's error instead of ending the bench."""
@@ -1558,7 +1565,7 @@ def prepare_datasets(args, extras):
             args._c4_meta = {"error": f"config-4 dataset: {e}"}
     if 3 in extras and args.c3_fastq_reads > 0:
         try:
-            args._c3f_meta = ensure_c3f_dataset(args)
+            args._c3f_meta = ensure_c3f_dataset(args, world)
         except (OSError, RuntimeError) as e:
             args._c3f_meta = {"error": f"config-3 FASTQ dataset: {e}"}
     for m in (args._c4_meta, args._c3f_meta):  # the record keeps the summary, not the per-file tables

@@ -101,9 +101,9 @@ def _check_extras(d, world):
     assert p["file0_ok"] is True and p["rows_ok"] is True and p["files_checked"] == 16
     assert c4["reads_per_s"] > 0 and c4["gcups"] > 0
     assert c4["segments"] == {**c4["segments"], "pool": 5, "segment_reads": 40, "segments_per_file": 3}
-    f3 = ex["config3"]["fastq"]  # per-read records of 16 lane files, gathered in file order
-    assert f3["n_ranks"] == world and f3["reads"] == 320
-    assert f3["parity"]["bit_exact"] is True and f3["parity"]["records_checked"] == 320
+    f3 = ex["config3"]["fastq"]  # per-read records of 2N lane files, gathered in file order
+    assert f3["n_ranks"] == world and f3["reads"] == 320 * world and f3["scaling"] == "weak"
+    assert f3["parity"]["bit_exact"] is True and f3["parity"]["records_checked"] == 320 * world
     col = d["collectives"]
     assert col["backend"] == "gloo" and col["world"] == world and col["calls_rank0"]["all_gather:int16->int32"] >= 1
 
