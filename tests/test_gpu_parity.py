@@ -241,6 +241,22 @@ def test_ctx_stats_count_kernel_time(gpu_ctx):
     assert gpu_ctx.stats()["launches"] == 0
 
 
+def test_ctx_stats_kernel_time_is_a_union(gpu_ctx):
+    """kernel_ms counts GPU time covered by scoring launches once: the chunks
+    of a multi-chunk call alternate two compute streams and overlap, so the
+    sum of their durations can exceed the call's wall time; the union cannot."""
+    import time
+    b = config_batch(2, n_pairs=40_000, seed_offset=43)
+    gpu_run(gpu_ctx, b, Scoring(), 4000)  # warm
+    gpu_ctx.stats(reset=True)
+    t0 = time.perf_counter()
+    gpu_run(gpu_ctx, b, Scoring(), 4000)
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    st = gpu_ctx.stats(reset=True)
+    assert st["launches"] >= 10 and st["pairs"] == 40_000
+    assert 0 < st["kernel_ms"] <= wall_ms, (st["kernel_ms"], wall_ms)
+
+
 def test_empty_batch(gpu_ctx):
     R = np.zeros((0, 16), np.uint8)
     s, i, j = gpu_ctx.align_batch(R, np.zeros(0, np.uint16), R, np.zeros(0, np.uint16), Scoring(want_coords=True))
