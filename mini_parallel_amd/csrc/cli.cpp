@@ -844,6 +844,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         return true;
                     }
                 };
+                // the first file too: opened and pinned on the reader's thread
+                // while the other workers finish their setup
+                pending = claim();
+                if (pending != kNone) (void)msw_gfastq_prefetch(gr, st[pending]->path.c_str());
                 gate.arrive();
                 // One loop over the batches of all of this worker's files: a
                 // file's last batches are settled after the next file's first
