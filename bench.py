@@ -929,8 +929,9 @@ def ensure_c4_dataset(args) -> dict:
 
 
 # config 3 from FASTQ (BASELINE: "1M synthetic 150 bp reads ... affine-gap
-# score + best-cell coord, async FASTQ chunk staging"): 16 lane files of
-# 62,500 reads, every read's (score, end_i, end_j) compared with the oracle.
+# score + best-cell coord, async FASTQ chunk staging"): 1 M reads per GPU in
+# one lane's R1/R2 BGZF files, every read's (score, end_i, end_j) compared
+# with the oracle.
 C3F_RPL, C3F_GENOME, C3F_SEED = 2, 64 << 20, 1003
 
 
