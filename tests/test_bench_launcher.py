@@ -157,3 +157,28 @@ def test_too_few_gpus_fails_loudly():
     assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
     assert "GPU(s) are visible" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("cfg,world", [(2, 2), (5, 3)])
+def test_parity_sample_covers_every_shard(cfg, world):
+    """bench.parity_sample (rank 0, N > 1, GPU runs): the sample it checks
+    comes from every rank's shard of the global batch, and it flags a wrong
+    score in any of them -- checked here with the oracle's own scores standing
+    in for the gathered GPU results."""
+    import bench
+    from oracle import oracle_lib
+    from mini_parallel_amd import dist as mdist
+    n_total = 700 * world
+    sc = bench.scoring_of(cfg)
+    b = config_shard(cfg, 0, n_total)
+    s, i, j, _ = oracle_lib.sw_batch_simd(b.reads, b.read_len, b.wins, b.win_len, threads=4,
+                                          coords=sc.want_coords, **bench._oracle_kw(sc))
+    par = bench.parity_sample(cfg, sc, n_total, world, s, i, j, per_shard=64)
+    assert par["bit_exact"] and par["checked_pairs"] == 64 * world
+    for (lo, hi), r in zip(par["checked_ranges"], range(world)):
+        a, bb = mdist.shard_range(n_total, r, world)
+        assert a <= lo < hi <= bb
+    lo, _ = par["checked_ranges"][-1]
+    bad = s.copy()
+    bad[lo] += 1  # one wrong score in the last shard's sample
+    assert bench.parity_sample(cfg, sc, n_total, world, bad, i, j, per_shard=64)["mismatches"] == 1
