@@ -123,6 +123,18 @@ def test_two_ranks_run_every_config(tmp_path, launch):
     _check_extras(d, 2)
 
 
+def test_eight_ranks_run_every_config(tmp_path):
+    """The driver's largest N: 8 ranks (gloo stand-in), every leg sharded and
+    gathered -- config 4's 16 lane files two per rank, config 3's FASTQ lane
+    per rank, configs 3 / 5 in order."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8"] + EXTRA + ["--c4-dir", str(tmp_path / "c4")],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    _check(d, 8, per_gpu=1000)
+    _check_extras(d, 8)
+
+
 def test_one_rank_runs_every_config(tmp_path):
     r = subprocess.run([sys.executable, "bench.py"] + EXTRA + ["--c4-dir", str(tmp_path / "c4")], cwd=ROOT,
                        env=_env(), capture_output=True, text=True, timeout=600)
