@@ -1076,6 +1076,22 @@ def _setup_split(rec):
 
 
 SETUP_PHASES = ("hip_init_ms", "reference_load_ms", "context_ms", "genome_ms", "result_sets_ms", "lane_reader_ms")
+# what each phase inside setup_ms is (named in the record when it binds)
+SETUP_WHY = {
+    "context_ms": "the HIP runtime's device bring-up in the process's first stream creation (HSA queue "
+                  "creation: 160-168 ms for the first hipStreamCreate on a fresh box, 2-14 ms for later ones, "
+                  "tools/setup_probe.cpp, profiles/r04/setup/setup_probe.jsonl); once per process, after the "
+                  "runtime init, so no call of ours can start it earlier",
+    "genome_ms": "each worker's copy of the reference into its context's HBM (pageable host memory)",
+    "result_sets_ms": "the workers' pinned host result buffers and their device twins",
+    "lane_reader_ms": "the GPU lane reader's span, inflate and parse buffers",
+}
+
+
+def _setup_bound(phases_ms):
+    """The phase inside setup_ms that takes longest, and what it is."""
+    k = max(SETUP_WHY, key=lambda n: phases_ms.get(n, 0.0))
+    return {"phase": k, "ms": phases_ms.get(k, 0.0), "why": SETUP_WHY[k]}
 
 
 def leg_config4(job, args):
@@ -1167,6 +1183,7 @@ def leg_config4(job, args):
            "wall_ms": round(wall_ms, 1), "setup_ms": round(setup_ms, 1), "teardown_ms": round(tear_ms, 1),
            "process_wall_ms": round(proc_ms, 1), "max_kernel_ms": round(kern_ms, 1),
            "setup_phases_ms": {k: round(v, 1) for k, v in zip(SETUP_PHASES, mx[6:])},
+           "setup_bound_by": _setup_bound(dict(zip(SETUP_PHASES, mx[6:]))),
            "timing": "wall_ms = the --full-wgs driver's timed region (workers set up -> last results on the "
                      "host), max over ranks; setup_ms = contexts, genome upload and reader buffers before it "
                      "(setup_phases_ms: each phase's max over workers and ranks; hip_init_ms comes before "
@@ -1303,6 +1320,7 @@ def leg_config3_fastq(job, args):
             "wall_ms": round(wall_ms, 1), "setup_ms": round(setup_ms, 1), "process_wall_ms": round(proc_ms, 1),
             "max_kernel_ms": round(kern_ms, 1),
             "setup_phases_ms": {k: round(v, 1) for k, v in zip(SETUP_PHASES, mx[6:])},
+            "setup_bound_by": _setup_bound(dict(zip(SETUP_PHASES, mx[6:]))),
             "parity": {"records_checked": checked, "records_expected": F * per, "mismatches": mism,
                        "files_done": files_ok,
                        "bit_exact": mism == 0 and checked == F * per and files_ok == F,

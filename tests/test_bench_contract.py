@@ -63,6 +63,9 @@ def test_bench_json_line(tmp_path):
     assert c4["parity"]["files_checked"] == 16 and c4["parity"]["files_mismatched"] == []
     assert c4["reads_per_s"] >= c4["reads_per_s_incl_setup"] > 0 and c4["setup_ms"] > 0
     assert c4["setup_phases_ms"]["context_ms"] > 0 and c4["setup_phases_ms"]["hip_init_ms"] > 0
+    sb = c4["setup_bound_by"]
+    assert sb["phase"] in c4["setup_phases_ms"] and sb["ms"] == max(
+        c4["setup_phases_ms"][k] for k in ("context_ms", "genome_ms", "result_sets_ms", "lane_reader_ms")) and sb["why"]
     assert c4["segments"]["segments_per_file"] == 2 and c4["segments"]["pool"] == 3
     # BASELINE config 3 from lane files: every per-read record against the oracle
     f3 = ex["config3"]["fastq"]
