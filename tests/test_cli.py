@@ -285,6 +285,41 @@ def test_full_wgs_file_shards(tmp_path, oracle):
 
 
 @pytest.mark.gpu
+def test_full_wgs_reference_formats(tmp_path, oracle):
+    """The reference FASTA (read on its own thread beside the HIP init): CRLF
+    line ends, a second header line splitting the sequence, blank lines and
+    ragged line widths give the same bases, so the same per-file sums as the
+    oracle's; a missing reference is refused with exit 1."""
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=1, reads_per_lane=2, reads_per_file=600, bgzf=True)
+    want = sum(int(oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=8)[0].astype(np.int64).sum())
+               for b in ds["batches"])
+    seq = "".join(l.strip() for l in open(ds["reference"]) if not l.startswith(">"))
+    cut = len(seq) // 3
+    odd = tmp_path / "odd.fa"
+    with open(odd, "wb") as f:
+        f.write(b">part one\r\n")
+        for k in range(0, cut, 61):
+            f.write(seq[k:min(k + 61, cut)].encode() + b"\r\n")
+        f.write(b"\r\n>part two\n\n")
+        rest = seq[cut:]
+        f.write("\n".join(rest[k:k + 97] for k in range(0, len(rest), 97)).encode())  # no final newline
+    env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "1",
+           "WGS_READS_PER_LANE": "2", "GPU_CHUNK_SIZE_READS": "300"}
+    for k, ref in enumerate([ds["reference"], str(odd)]):
+        r = run(["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ref, "--window", "300",
+                 "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / f"rec{k}.json")],
+                env=dict(env, WGS_RUN_ID=f"ref{k}"), cwd=tmp_path)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert f"Loaded reference: {len(seq)} bases" in r.stdout
+        rec = json.load(open(tmp_path / f"rec{k}.json"))
+        assert rec["total_score"] == want and rec["setup_phases"]["reference_load_ms"] > 0
+    r = run(["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", str(tmp_path / "missing.fa")],
+            env=env, cwd=tmp_path)
+    assert r.returncode == 1 and "cannot open reference" in r.stderr
+
+
+@pytest.mark.gpu
 def test_num_gpus_beyond_visible_fails(tmp_path):
     from mini_parallel_amd.synthetic import write_wgs_dataset
     import torch
