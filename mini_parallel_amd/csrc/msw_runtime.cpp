@@ -1052,8 +1052,8 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         s.out = *out;
         if (!sch.coords) { s.out.end_i = nullptr; s.out.end_j = nullptr; }
     }
+    if (tr.on) tr.submit += tr.lap();  // the last chunk's HIP calls
     if (sync) {
-        if (tr.on) tr.submit += tr.lap();
         for (Slot& sl : ctx->slots)
             if ((rc = drain_slot(ctx, sl))) return rc;
         if (tr.on) tr.wait += tr.lap();
