@@ -1194,8 +1194,8 @@ def leg_config4(job, args):
            "timing": "wall_ms = the --full-wgs driver's timed region (workers set up -> last results on the "
                      "host), max over ranks; setup_ms = contexts, genome upload and reader buffers before it "
                      "(setup_phases_ms: each phase's max over workers and ranks; hip_init_ms comes before "
-                     "setup_ms, reference_load_ms runs on its own thread beside hip_init_ms and the "
-                     "contexts); process_wall_ms = the rank's child process "
+                     "setup_ms, reference_load_ms runs on its own thread beside hip_init_ms); "
+                     "process_wall_ms = the rank's child process "
                      "start to exit",
            "segments": {"pool": P, "segment_reads": S, "segments_per_file": R // S,
                         "distinct_reads": P * S, "note": "lane files are concatenations of pooled, pre-scored "

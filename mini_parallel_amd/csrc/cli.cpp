@@ -53,10 +53,14 @@ double ms_since(Clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
 }
 
+// Exit 1 with a message.  _exit: a worker thread may die while others are
+// still inside HIP calls, and exit()'s static destructors (the HIP runtime's
+// teardown) would race them.
 [[noreturn]] void die(const std::string& msg) {
     fflush(stdout);
     fprintf(stderr, "%s\n", msg.c_str());
-    exit(1);
+    fflush(stderr);
+    _exit(1);
 }
 
 std::string env_or(const char* k, const std::string& d) {
@@ -318,8 +322,7 @@ bool load_fasta(const std::string& path, std::string* seq) {
 }
 
 // The reference, loaded on a thread of its own from the start of main, beside
-// the HIP runtime init and the workers' contexts; the workers wait for it
-// only at their genome upload.
+// the HIP runtime init; run_full_wgs takes it before the workers start.
 struct ReferenceLoad {
     std::string path, seq;
     double ms = 0;
@@ -600,8 +603,8 @@ struct WgsReport {
     double teardown_ms = 0;        // release after the last results, outside the clock
     // setup split (JSON "setup_phases", each phase's max over the workers):
     // reference_load on its own thread from the start of main, beside hip_init
-    // and the contexts (a worker that reaches its genome upload first waits,
-    // inside genome); context / genome upload / result sets / lane reader
+    // (run_full_wgs waits for it before setup); context / genome upload /
+    // result sets / lane reader
     // inside setup_ms (workers run them side by side); hip_init is filled in
     // by main (the first HIP call, before setup_ms)
     double reference_load_ms = 0, context_ms = 0, genome_ms = 0, result_sets_ms = 0, lane_reader_ms = 0;
@@ -660,13 +663,11 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         rep.lane_reader_ms = ph_reader;
     };
     if (sw && a.reference.empty()) die("error: --score-mode sw with --full-wgs needs --reference <FASTA>");
-    // the reference's bases, waited for at the first genome upload
-    std::once_flag ref_msg;
-    auto genome = [&]() -> const std::string& {
-        const std::string& g = ref.get();
-        std::call_once(ref_msg, [&]() { printf("Loaded reference: %zu bases\n", g.size()); });
-        return g;
-    };
+    // the reference: loading since the top of main, beside the HIP runtime
+    // init (which takes longer), so this wait is normally over at once; a
+    // reference that cannot be read fails here, before any worker starts
+    if (sw) printf("Loaded reference: %zu bases\n", ref.get().size());
+    auto genome = [&]() -> const std::string& { return ref.get(); };
     const int ngpu = (int)devices.size();  // already worker_devices(): one worker per entry
     std::vector<msw_stats_t> gstats((size_t)ngpu);
     std::vector<std::unique_ptr<FileState>> st(files.size());
@@ -1258,8 +1259,8 @@ void write_json(const std::string& path, const std::string& body) {
 int main(int argc, char** argv) {
     load_dotenv();
     const Args a = parse_args(argc, argv);
-    // --full-wgs sw: the reference loads beside the HIP runtime init and the
-    // workers' contexts (setup_phases.reference_load_ms is its own duration)
+    // --full-wgs sw: the reference loads beside the HIP runtime init
+    // (setup_phases.reference_load_ms is its own duration)
     ReferenceLoad ref;
     if (a.full_wgs && a.score_mode == "sw" && !a.reference.empty()) ref.start(a.reference);
     const auto t_hip = Clock::now();

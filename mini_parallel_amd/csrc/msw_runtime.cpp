@@ -935,9 +935,14 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     if (tr.on) tr.scan += tr.lap();
 
     const uint64_t chunk = chunk_pairs ? chunk_pairs : default_chunk();
-    // Copies go on the copy stream (overlapping the previous chunk's kernels)
-    // unless a synchronous one-chunk call has nothing to overlap with.
-    const bool multi_chunk = n > chunk || !sync;
+    // A multi-chunk call pipelines its own chunks: copies on the copy stream,
+    // kernels alternating between the two compute streams, results back on
+    // the d2h stream.  A one-chunk call keeps all of its work on one compute
+    // stream (no cross-stream events: ~5 HIP calls fewer per call, the host
+    // cost that bounds a stream of small async batches); async calls
+    // alternate that stream, so consecutive calls still overlap.
+    const bool multi_chunk = n > chunk;
+    const bool alternate = multi_chunk || !sync;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
@@ -948,7 +953,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         // Slots alternate across calls too, so consecutive async calls overlap.
         const uint64_t seq = ctx->slot_seq++;
         Slot& s = ctx->slots[seq % msw_ctx::kSlots];
-        hipStream_t cs = (multi_chunk && (seq & 1)) ? ctx->compute2 : ctx->compute;
+        hipStream_t cs = (alternate && (seq & 1)) ? ctx->compute2 : ctx->compute;
         if (tr.on) tr.submit += tr.lap();
         if ((rc = drain_slot(ctx, s))) return rc;  // the slot's previous chunk must be out before reuse
         if (tr.on) tr.wait += tr.lap();
@@ -998,8 +1003,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         }
         if (tr.on) tr.stage += tr.lap();
         // H2D on the copy stream, kernels on the compute stream (a one-chunk
-        // batch has nothing to overlap: everything goes on the compute stream,
-        // saving the cross-stream event).
+        // call: everything on its compute stream).
         hipStream_t up = multi_chunk ? ctx->copy : cs;
         HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
         if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
