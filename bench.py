@@ -1098,7 +1098,7 @@ SETUP_WHY = {
 def _setup_bound(phases_ms):
     """The phase inside setup_ms that takes longest, and what it is."""
     k = max(SETUP_WHY, key=lambda n: phases_ms.get(n, 0.0))
-    return {"phase": k, "ms": phases_ms.get(k, 0.0), "why": SETUP_WHY[k]}
+    return {"phase": k, "ms": round(phases_ms.get(k, 0.0), 1), "why": SETUP_WHY[k]}
 
 
 def leg_config4(job, args):
