@@ -552,13 +552,13 @@ struct Bucket {
     bool spread = false;      // long pairs of spread lengths, sorted heaviest first
 };
 
+// lengths: the chunk's {min read, max read, min window, max window}.
 void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32_t* order,
-                  std::vector<Bucket>& buckets) {
+                  std::vector<Bucket>& buckets, uint32_t lengths[4]) {
     buckets.clear();
     // key = KR (1..24) * 257 + ceil(n / 16) (<= 256): counting sort; pairs
     // beyond the packed kernels' limits share the last key.
     constexpr int kLongKey = (msw::kMaxRowsPerLane + 1) * 257, kKeys = kLongKey + 1;
-    std::vector<uint32_t> hist(kKeys + 1, 0);
     const bool all_long = force_long();
     auto key_of = [&](uint64_t i) {
         if (all_long || is_long(rlen[i], wlen[i])) return kLongKey;
@@ -580,12 +580,14 @@ void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32
         lm = std::min<uint32_t>(lm, rlen[i]);
         ln = std::min<uint32_t>(ln, wlen[i]);
     }
+    lengths[0] = lm, lengths[1] = gm, lengths[2] = ln, lengths[3] = gn;
     const bool spread_long = kmin == kLongKey && (gm - lm >= 64 || gn - ln >= 64);
     if (n && kmin == kmax && !spread_long) {
         for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
         buckets.push_back({0, (uint32_t)n, gm, gn, kmin == kLongKey});
         return;
     }
+    std::vector<uint32_t> hist(kKeys + 1, 0);
     for (uint64_t i = 0; i < n; ++i) hist[key_of(i) + 1]++;
     for (int k = 0; k < kKeys; ++k) hist[k + 1] += hist[k];
     std::vector<uint32_t> pos(hist.begin(), hist.end() - 1);
@@ -979,28 +981,20 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         if (gmode) {
             const int64_t* p = b.win_pos + first;
             const uint16_t* req = b.win_len + first;
-            for (uint64_t i = 0; i < cnt; ++i) s.h_wlen[i] = genome_window(p[i], req[i], b.genome->len);
-            memcpy(s.h_pos, p, cnt * sizeof(int64_t));
+            const uint64_t glen = b.genome->len;
+            for (uint64_t i = 0; i < cnt; ++i) {
+                s.h_pos[i] = p[i];
+                s.h_wlen[i] = genome_window(p[i], req[i], glen);
+            }
         } else {
             memcpy(s.h_wlen, b.win_len + first, cnt * sizeof(uint16_t));
         }
-        bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets);
-        bool uniform = buckets.size() == 1;
-        if (uniform) {
-            // One read-length bucket: order only matters if windows vary a lot.
-            uint32_t mn = 0xFFFF, mx = 0;
-            for (uint64_t i = 0; i < cnt; ++i) {
-                mn = std::min<uint32_t>(mn, s.h_wlen[i]);
-                mx = std::max<uint32_t>(mx, s.h_wlen[i]);
-            }
-            uniform = (mx - mn) < 16;
-            // long pairs of spread read lengths keep their heaviest-first order
-            if (buckets[0].long_pairs) {
-                uint32_t lo = 0xFFFF;
-                for (uint64_t i = 0; i < cnt; ++i) lo = std::min<uint32_t>(lo, s.h_rlen[i]);
-                uniform = uniform && buckets[0].max_m - lo < 64;
-            }
-        }
+        uint32_t lens[4];
+        bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets, lens);
+        // One read-length bucket: order only matters if windows vary a lot;
+        // long pairs of spread read lengths keep their heaviest-first order.
+        const bool uniform = buckets.size() == 1 && lens[3] - lens[2] < 16 &&
+                             (!buckets[0].long_pairs || lens[1] - lens[0] < 64);
         if (tr.on) tr.stage += tr.lap();
         // H2D on the copy stream, kernels on the compute stream (a one-chunk
         // call: everything on its compute stream).
@@ -1392,7 +1386,8 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
     if (n_pairs) {
         std::vector<uint32_t> order(n_pairs);
         std::vector<Bucket> buckets;
-        bucket_chunk(read_len, win_len, n_pairs, order.data(), buckets);
+        uint32_t lens[4];
+        bucket_chunk(read_len, win_len, n_pairs, order.data(), buckets, lens);
         const size_t n_short = short_buckets(buckets);
         if (n_short < buckets.size()) {
             pl->has_long = true;
