@@ -272,13 +272,6 @@ struct msw_ctx {
     // compute2, so chunk k+1's waves start under chunk k's tail (one stream
     // would idle the CUs the tail leaves)
     hipStream_t compute2 = nullptr;
-    // one-chunk async calls rotate over compute, compute2 and compute3 (call k
-    // on stream k % 3, the stream of its slot): with three calls in flight a
-    // call's uploads start when it is submitted, not behind the kernel of the
-    // call two before it on a shared stream (created at the first such call:
-    // contexts that never make one, like the --full-wgs GPU reader's, skip
-    // its creation cost at setup)
-    hipStream_t compute3 = nullptr;
     hipStream_t side = nullptr;  // long-pair launches beside packed ones (fork_side)
     // Staging slots, used round robin by successive chunks (and calls): with
     // three, the host stages chunk k+1 while k runs and k-1 drains, so the
@@ -948,9 +941,10 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     // kernels alternating between the two compute streams, results back on
     // the d2h stream.  A one-chunk call keeps all of its work on one compute
     // stream (no cross-stream events: ~5 HIP calls fewer per call, the host
-    // cost that bounds a stream of small async batches); async calls rotate
-    // over three compute streams, so consecutive calls still overlap.
+    // cost that bounds a stream of small async batches); async calls
+    // alternate that stream, so consecutive calls still overlap.
     const bool multi_chunk = n > chunk;
+    const bool alternate = multi_chunk || !sync;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
@@ -961,11 +955,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         // Slots alternate across calls too, so consecutive async calls overlap.
         const uint64_t seq = ctx->slot_seq++;
         Slot& s = ctx->slots[seq % msw_ctx::kSlots];
-        if (!multi_chunk && !sync && !ctx->compute3)
-            HIP_TRY(hipStreamCreateWithFlags(&ctx->compute3, hipStreamNonBlocking));
-        const hipStream_t rot[msw_ctx::kSlots] = {ctx->compute, ctx->compute2, ctx->compute3};
-        hipStream_t cs = multi_chunk ? ((seq & 1) ? ctx->compute2 : ctx->compute)
-                                     : (sync ? ctx->compute : rot[seq % msw_ctx::kSlots]);
+        hipStream_t cs = (alternate && (seq & 1)) ? ctx->compute2 : ctx->compute;
         if (tr.on) tr.submit += tr.lap();
         if ((rc = drain_slot(ctx, s))) return rc;  // the slot's previous chunk must be out before reuse
         if (tr.on) tr.wait += tr.lap();
@@ -1096,7 +1086,6 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
         (void)hipStreamSynchronize(ctx->copy);
         (void)hipStreamSynchronize(ctx->compute);
         (void)hipStreamSynchronize(ctx->compute2);
-        if (ctx->compute3) (void)hipStreamSynchronize(ctx->compute3);
         (void)hipStreamSynchronize(ctx->d2h);
         (void)hipStreamSynchronize(ctx->side);
         for (Slot& s : ctx->slots)
@@ -1209,7 +1198,6 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->compute) (void)hipStreamSynchronize(ctx->compute);
     if (ctx->compute2) (void)hipStreamSynchronize(ctx->compute2);
-    if (ctx->compute3) (void)hipStreamSynchronize(ctx->compute3);
     if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
     if (ctx->d2h) (void)hipStreamSynchronize(ctx->d2h);
     if (ctx->side) (void)hipStreamSynchronize(ctx->side);
@@ -1237,7 +1225,6 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     if (ctx->epoch) (void)hipEventDestroy(ctx->epoch);
     if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
     if (ctx->compute2) (void)hipStreamDestroy(ctx->compute2);
-    if (ctx->compute3) (void)hipStreamDestroy(ctx->compute3);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -1782,7 +1769,6 @@ int msw_synchronize(msw_ctx* ctx) {
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->compute));
     HIP_TRY(hipStreamSynchronize(ctx->compute2));
-    if (ctx->compute3) HIP_TRY(hipStreamSynchronize(ctx->compute3));
     HIP_TRY(hipStreamSynchronize(ctx->copy));
     HIP_TRY(hipStreamSynchronize(ctx->d2h));
     HIP_TRY(hipGetLastError());
