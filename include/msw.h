@@ -104,7 +104,9 @@ void msw_ctx_destroy(msw_ctx* ctx);
 
 /* Batched scoring from host memory, synchronous.  Streams the batch through
  * pinned staging in chunks of `chunk_pairs` (0 = GPU_CHUNK_SIZE_READS env, or
- * 65536) with H2D copies on the copy stream overlapped with the kernels.
+ * 65536) with H2D copies on the copy stream overlapped with the kernels (a
+ * one-chunk call keeps its copies and kernels on one compute stream; async
+ * one-chunk calls alternate two, so consecutive calls overlap).
  * Pageable arrays are staged (rows repacked to 16-byte-rounded strides, so
  * padding does not cross PCIe); arrays in pinned memory (msw_host_alloc or
  * hipHostRegister) are copied to the GPU directly.
