@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 for span in 1024 256 128 64 32; do
   for rep in 1 2; do
     MSW_GFASTQ_SPAN_MB=$span timeout -k 10 200 python3 bench.py --steps 2 --warmup 1 --pairs 2000 --cpu-seconds 0 \
-      --no-pcie --no-h2h --extra-configs 3 --c3-pairs 2000 --c3-fastq-lanes 1 2>/dev/null | grep '^{' | python3 -c "
+      --no-pcie --no-h2h --extra-configs 3 --c3-pairs 2000 2>/dev/null | grep '^{' | python3 -c "
 import json, sys
 d = json.loads(sys.stdin.read())['configs_extra']['config3']['fastq']
 print(json.dumps({'span_mb': $span, 'reads_per_s': d['reads_per_s'], 'wall_ms': d['wall_ms'],
