@@ -759,6 +759,22 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 const auto ts0 = Clock::now();
                 Ctx ctx(devices[gi].ordinal);
                 const double t_ctx = ms_since(ts0);
+                msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
+                if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
+                    die(std::string("GPU lane reader: ") + msw_last_error());
+                const double t_rd = ms_since(ts0);
+                const size_t kNone = ~(size_t)0;
+                size_t pending = kNone;
+                auto claim = [&]() -> size_t {
+                    const size_t k = next_file.fetch_add(1);
+                    return k < todo.size() ? todo[k] : kNone;
+                };
+                // the first file: claimed now and opened / pinned on the
+                // reader's thread (msw_gfastq_prefetch) while this worker
+                // uploads the genome and allocates its result sets, so its
+                // first window is ready when the clock starts
+                pending = claim();
+                if (pending != kNone) (void)msw_gfastq_prefetch(gr, st[pending]->path.c_str());
                 const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
                 msw_genome* gen = nullptr;
                 const std::string& ref_seq = genome();
@@ -840,11 +856,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     maybe_finish(r.fi);
                 };
                 int cur = 0;
-                msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
-                const double t_res = ms_since(ts0);
-                if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
-                    die(std::string("GPU lane reader: ") + msw_last_error());
-                setup_phase(t_ctx, t_gen - t_ctx, t_res - t_gen, ms_since(ts0) - t_res);
+                setup_phase(t_ctx, t_gen - t_rd, ms_since(ts0) - t_gen, t_rd - t_ctx);
                 // the reader's stats of the file it just finished
                 auto reader_done = [&](size_t fi) {
                     uint64_t bi = 0, bo = 0;
@@ -860,12 +872,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 // left.  The worker claims the file after it at the same time
                 // and has the reader pin that file's first window now
                 // (msw_gfastq_prefetch), so the next switch does not wait on it.
-                const size_t kNone = ~(size_t)0;
-                size_t pending = kNone;
-                auto claim = [&]() -> size_t {
-                    const size_t k = next_file.fetch_add(1);
-                    return k < todo.size() ? todo[k] : kNone;
-                };
                 auto open_next = [&](size_t* fi_out) -> bool {
                     for (;;) {
                         const size_t fi = pending != kNone ? pending : claim();
@@ -898,10 +904,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         return true;
                     }
                 };
-                // the first file too: opened and pinned on the reader's thread
-                // while the other workers finish their setup
-                pending = claim();
-                if (pending != kNone) (void)msw_gfastq_prefetch(gr, st[pending]->path.c_str());
                 gate.arrive();
                 // One loop over the batches of all of this worker's files: a
                 // file's last batches are settled after the next file's first
