@@ -559,10 +559,12 @@ int next_span(msw_gfastq* g) {
     const double t0 = trace ? now_ms() : 0.0;
     const int nx = 1 - g->last_buf;
     join_filler(g);
+    const double t_join = trace ? now_ms() : 0.0;
     if (g->fill_rc) return set_error(g->fill_rc, "%s", g->fill_msg.c_str());
     if (g->mapped && g->reg_failed && (rc = to_copied(g))) return rc;
     if (g->mapped && !g->reg_len && g->map_off < g->fsize) register_window(g);  // no read-ahead ran
     if (g->mapped && g->reg_failed && (rc = to_copied(g))) return rc;
+    const double t_reg = trace ? now_ms() : 0.0;
     // A lane file must not change while it is read (the mapping is
     // MAP_SHARED: touching pages past a truncation raises SIGBUS).  Checked
     // before the host parses this span's member headers, so a file truncated
@@ -676,10 +678,11 @@ int next_span(msw_gfastq* g) {
     GZ_TRY(hipStreamSynchronize(s));
     const msw::ParseOut& o = *g->h_out;
     if (trace)
-        fprintf(stderr, "[gfastq] %s span: %zu members, %.1f MB in, %.1f MB out: read+index %.2f ms, "
+        fprintf(stderr, "[gfastq] %s span: %zu members, %.1f MB in, %.1f MB out: read+index %.2f ms "
+                        "(read-ahead join %.2f, window pin %.2f, index %.2f), "
                         "inflate+parse A %.2f ms, parse B %.2f ms, %llu reads\n",
-                g->path.c_str(), g->mem.size(), used / 1e6, obytes / 1e6, t_read - t0, t_a - t_read, now_ms() - t_a,
-                (unsigned long long)o.reads);
+                g->path.c_str(), g->mem.size(), used / 1e6, obytes / 1e6, t_read - t0, t_join - t0, t_reg - t_join,
+                t_read - t_reg, t_a - t_read, now_ms() - t_a, (unsigned long long)o.reads);
     if (o.err_over)
         return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
                          (unsigned long long)o.err_line);
