@@ -309,8 +309,20 @@ struct msw_gfastq {
         uint64_t fsize = 0, reg_len = 0;
         uint8_t* map = nullptr;
         bool ok = false;
+        // the first span's member index, built on the same thread (the host
+        // walk over the window's member headers; its page touches stalled the
+        // reader up to ~20 ms beside other threads' pinning)
+        std::vector<msw::GzMember> mem;
+        size_t used = 0;
+        uint64_t obytes = 0;
+        bool indexed = false;
         std::thread th;
     } pf;
+    // a prefetched file's first span, indexed ahead (open_file adopts it)
+    std::vector<msw::GzMember> pre_mem;
+    size_t pre_used = 0;
+    uint64_t pre_obytes = 0;
+    bool pre_indexed = false;
     // read-ahead: while the GPU inflates / the caller scores, a host thread
     // reads the next span's compressed bytes into hc after hc_len
     std::thread filler;
@@ -378,6 +390,8 @@ void drop_prefetch(msw_gfastq* g) {
     p.map = nullptr;
     p.fsize = p.reg_len = 0;
     p.ok = false;
+    p.indexed = false;
+    p.mem.clear();
     p.path.clear();
 }
 
@@ -584,12 +598,19 @@ int next_span(msw_gfastq* g) {
     // 16 files, 67-69 vs 76 M over 2 files (profiles/r03/e2e/first_span_ab.jsonl):
     // fewer members per inflate launch cost more than the earlier start wins.
     const uint64_t cap = g->span;
-    for (;;) {
-        if ((rc = index_members(g->hc, g->hc_len, kCarry, cap, g->in_cap, g->mem, &used, &obytes))) return rc;
-        const bool full = obytes + 65536 > cap || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
-        if (full) break;
-        g->mem.clear();
-        if ((rc = fill_compressed(g, g->hc_len + kReadPiece))) return rc;
+    if (g->pre_indexed) {  // a prefetched file's first span: indexed on the prefetch thread
+        g->mem.swap(g->pre_mem);
+        used = g->pre_used;
+        obytes = g->pre_obytes;
+        g->pre_indexed = false;
+    } else {
+        for (;;) {
+            if ((rc = index_members(g->hc, g->hc_len, kCarry, cap, g->in_cap, g->mem, &used, &obytes))) return rc;
+            const bool full = obytes + 65536 > cap || g->fread_off >= g->fsize || g->hc_len == g->hc_cap;
+            if (full) break;
+            g->mem.clear();
+            if ((rc = fill_compressed(g, g->hc_len + kReadPiece))) return rc;
+        }
     }
     const bool last = g->fread_off >= g->fsize && used == g->hc_len;
     if (g->mem.empty() && !last) {
@@ -743,6 +764,7 @@ int open_file(msw_gfastq* g, const char* path) {
     g->fill_rc = 0;
     g->last_used = 0;
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
+    g->pre_indexed = false;
     if (g->pf.ok && g->pf.path == path) {
         // prefetched (msw_gfastq_prefetch): file open, mapped, first window
         // [0, reg_len) pinned -- the state register_window leaves behind
@@ -756,10 +778,18 @@ int open_file(msw_gfastq* g, const char* path) {
         g->hc = g->map;
         g->hc_len = g->hc_cap = (size_t)p.reg_len;
         g->fread_off = p.reg_len;
+        if (p.indexed) {
+            g->pre_mem.swap(p.mem);
+            g->pre_used = p.used;
+            g->pre_obytes = p.obytes;
+            g->pre_indexed = true;
+        }
         p.f = nullptr;
         p.map = nullptr;
         p.fsize = p.reg_len = 0;
         p.ok = false;
+        p.indexed = false;
+        p.mem.clear();
         p.path.clear();
         if (g->d_state) {
             GZ_TRY(hipSetDevice(g->device));
@@ -901,10 +931,11 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
     if (nm && atoi(nm) != 0) return MSW_OK;  // copied mode: nothing to pin ahead
     g->pf.path = path;
     const size_t cap = g->in_cap;
+    const uint64_t span = g->span;
     const int device = g->device;
     msw_gfastq::Prefetch* p = &g->pf;
     try {
-        p->th = std::thread([p, cap, device]() {
+        p->th = std::thread([p, cap, span, device]() {
             // any failure leaves ok = false: reset then opens the file the usual way
             p->f = fopen(p->path.c_str(), "rb");
             if (!p->f) return;
@@ -927,6 +958,11 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
             }
             p->reg_len = hi;
             p->ok = true;
+            // the first span's members, as next_span would index them for a
+            // fresh file (hc = the window, full on the first pass); an error
+            // leaves it to next_span, which reports it
+            p->mem.clear();
+            p->indexed = index_members(p->map, (size_t)hi, kCarry, span, cap, p->mem, &p->used, &p->obytes) == 0;
         });
     } catch (const std::exception&) {
         g->pf.path.clear();  // no thread to spare: reset opens it then
