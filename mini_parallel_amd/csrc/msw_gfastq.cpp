@@ -192,14 +192,19 @@ struct Inflater {
         h_flag = nullptr;
     }
     // upload cbytes of compressed data + the member table, inflate into out, check CRCs
+    // d_pre: the compressed bytes already on the device (cbytes + kInPad, the
+    // pad zeroed; the caller orders s after their upload), no upload here
     int run(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, uint8_t* out,
-            hipStream_t s) {
+            hipStream_t s, const uint8_t* d_pre = nullptr) {
         int rc;
-        if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
         if ((rc = grow(&d_mem, &mem_cap, mem.size()))) return rc;
         if ((rc = grow(&d_status, &status_cap, mem.size()))) return rc;
-        if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
-        GZ_TRY(hipMemsetAsync(dc + cbytes, 0, kInPad, s));
+        if (!d_pre) {
+            if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
+            if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
+            GZ_TRY(hipMemsetAsync(dc + cbytes, 0, kInPad, s));
+        }
+        const uint8_t* src = d_pre ? d_pre : dc;
         if (!mem.empty())
             GZ_TRY(hipMemcpyAsync(d_mem, mem.data(), mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
         GZ_TRY(hipMemsetAsync(d_flag, 0, 4, s));
@@ -217,7 +222,7 @@ struct Inflater {
         uint32_t* d_prof = nullptr;
         if (prof_on && n) GZ_TRY(hipMalloc((void**)&d_prof, (size_t)n * 64));
         if (d_prof) GZ_TRY(hipMemsetAsync(d_prof, 0, (size_t)n * 64, s));
-        GZ_TRY(msw::launch_gz_inflate(dc, d_mem, n, out, d_status, d_flag, s, d_prof));
+        GZ_TRY(msw::launch_gz_inflate(src, d_mem, n, out, d_status, d_flag, s, d_prof));
         if (timing) GZ_TRY(hipEventRecord(ev[1], s));
         if (d_prof) {
             std::vector<uint32_t> h((size_t)n * 16);
@@ -316,8 +321,19 @@ struct msw_gfastq {
         size_t used = 0;
         uint64_t obytes = 0;
         bool indexed = false;
+        bool uploaded = false;  // that span copied to pre_dc (preupload_next)
         std::thread th;
     } pf;
+    // The prefetched file's first span on the device: copied on stream us at
+    // this file's last span (preupload_next), so the next file's first
+    // inflate does not wait on PCIe; pre_done orders the next copy after the
+    // inflate that read it
+    uint8_t* pre_dc = nullptr;
+    size_t pre_dc_cap = 0;
+    hipStream_t us = nullptr;
+    hipEvent_t pre_up = nullptr, pre_done = nullptr;
+    bool pre_done_valid = false;
+    bool pre_uploaded = false;  // the adopted file's first span is in pre_dc
     // a prefetched file's first span, indexed ahead (open_file adopts it)
     std::vector<msw::GzMember> pre_mem;
     size_t pre_used = 0;
@@ -383,6 +399,7 @@ void join_prefetch(msw_gfastq* g) {
 void drop_prefetch(msw_gfastq* g) {
     join_prefetch(g);
     msw_gfastq::Prefetch& p = g->pf;
+    if (p.uploaded && g->us) (void)hipStreamSynchronize(g->us);  // the copy reads the pinned window
     if (p.reg_len) (void)hipHostUnregister(p.map);
     if (p.map) munmap(p.map, (size_t)p.fsize);
     if (p.f) fclose(p.f);
@@ -391,17 +408,62 @@ void drop_prefetch(msw_gfastq* g) {
     p.fsize = p.reg_len = 0;
     p.ok = false;
     p.indexed = false;
+    p.uploaded = false;
     p.mem.clear();
     p.path.clear();
+}
+
+// At this file's last span (its own upload done): the prefetched next file's
+// first span -- pinned and indexed on the prefetch thread -- goes to the
+// device on stream us, beside this span's inflate, parse and scoring.  Any
+// failure leaves it to next_span's own upload.
+void preupload_next(msw_gfastq* g) {
+    msw_gfastq::Prefetch& p = g->pf;
+    if (p.path.empty() || p.uploaded) return;
+    join_prefetch(g);
+    if (!p.ok || !p.indexed || !p.used) return;
+    if (!g->us && hipStreamCreateWithFlags(&g->us, hipStreamNonBlocking) != hipSuccess) {
+        g->us = nullptr;
+        (void)hipGetLastError();
+        return;
+    }
+    if (!g->pre_up && (hipEventCreateWithFlags(&g->pre_up, hipEventDisableTiming) != hipSuccess ||
+                       hipEventCreateWithFlags(&g->pre_done, hipEventDisableTiming) != hipSuccess)) {
+        (void)hipGetLastError();
+        return;
+    }
+    if (g->pre_done_valid && hipStreamWaitEvent(g->us, g->pre_done, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    if (p.used + kInPad > g->pre_dc_cap) {
+        // a larger buffer: the previous one's readers finish first (hipFree waits)
+        if (grow(&g->pre_dc, &g->pre_dc_cap, p.used + kInPad)) return;
+    }
+    if (hipMemcpyAsync(g->pre_dc, p.map, p.used, hipMemcpyHostToDevice, g->us) != hipSuccess ||
+        hipMemsetAsync(g->pre_dc + p.used, 0, kInPad, g->us) != hipSuccess ||
+        hipEventRecord(g->pre_up, g->us) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(g->us);
+        return;
+    }
+    p.uploaded = true;
 }
 
 void unmap_file(msw_gfastq* g);
 
 void release(msw_gfastq* g) {
     join_filler(g);
-    drop_prefetch(g);
     (void)hipSetDevice(g->device);
+    drop_prefetch(g);
     if (g->rs) (void)hipStreamSynchronize(g->rs);
+    if (g->us) {
+        (void)hipStreamSynchronize(g->us);
+        (void)hipStreamDestroy(g->us);
+    }
+    if (g->pre_up) (void)hipEventDestroy(g->pre_up);
+    if (g->pre_done) (void)hipEventDestroy(g->pre_done);
+    if (g->pre_dc) (void)hipFree(g->pre_dc);
     unmap_file(g);
     if (g->f) fclose(g->f);
     for (int i = 0; i < 2; ++i) {
@@ -632,7 +694,14 @@ int next_span(msw_gfastq* g) {
     const size_t lead = g->mapped ? (size_t)(g->map_off - g->reg_lo) : 0;
     if (lead)
         for (msw::GzMember& m : g->mem) m.coff += lead;
-    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s))) return rc;
+    const bool pre = g->pre_uploaded;  // a prefetched first span already on the device
+    g->pre_uploaded = false;
+    if (pre) GZ_TRY(hipStreamWaitEvent(s, g->pre_up, 0));
+    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s, pre ? g->pre_dc : nullptr))) return rc;
+    if (pre) {
+        GZ_TRY(hipEventRecord(g->pre_done, s));
+        g->pre_done_valid = true;
+    }
     // 3. the previous span's unfinished line goes right in front
     const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
     if (carry > kCarry)
@@ -665,6 +734,7 @@ int next_span(msw_gfastq* g) {
     if (lead)  // uploads done: the member table holds offsets into hc again
         for (msw::GzMember& m : g->mem) m.coff -= lead;
     if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
+    if (last) preupload_next(g);
     // the upload of hc has completed: drop the consumed bytes and read ahead
     if (g->mapped) {
         // the window's upload is done: unpin it; the next one registers in the background
@@ -742,9 +812,11 @@ int open_file(msw_gfastq* g, const char* path) {
     join_filler(g);
     join_prefetch(g);
     if (g->mapped || g->map) {
-        // the previous file's last window may still be uploading
+        // the previous file's last window may still be uploading (and its
+        // first span's pre-upload, when it was never read)
         GZ_TRY(hipSetDevice(g->device));
         GZ_TRY(hipStreamSynchronize(g->rs));
+        if (g->us) GZ_TRY(hipStreamSynchronize(g->us));
         unmap_file(g);
     }
     if (g->f) fclose(g->f);
@@ -764,7 +836,7 @@ int open_file(msw_gfastq* g, const char* path) {
     g->fill_rc = 0;
     g->last_used = 0;
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
-    g->pre_indexed = false;
+    g->pre_indexed = g->pre_uploaded = false;
     if (g->pf.ok && g->pf.path == path) {
         // prefetched (msw_gfastq_prefetch): file open, mapped, first window
         // [0, reg_len) pinned -- the state register_window leaves behind
@@ -783,12 +855,14 @@ int open_file(msw_gfastq* g, const char* path) {
             g->pre_used = p.used;
             g->pre_obytes = p.obytes;
             g->pre_indexed = true;
+            g->pre_uploaded = p.uploaded;
         }
         p.f = nullptr;
         p.map = nullptr;
         p.fsize = p.reg_len = 0;
         p.ok = false;
         p.indexed = false;
+        p.uploaded = false;
         p.mem.clear();
         p.path.clear();
         if (g->d_state) {

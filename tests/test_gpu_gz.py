@@ -272,6 +272,32 @@ def test_reader_prefetch_next_file(gpu_ctx, tmp_path, monkeypatch, mode):
         assert np.array_equal(hl, gl) and np.array_equal(hp, gp) and np.array_equal(hs, gs), f
 
 
+@pytest.mark.parametrize("span", [1 << 20, 1 << 18])
+def test_reader_prefetch_chain(gpu_ctx, tmp_path, monkeypatch, span):
+    """Lane files read back to back, each with the next one prefetched (the
+    --full-wgs worker's order): at a file's last span the next file's first
+    span is copied to the device ahead (one buffer, reused file after file,
+    its reuse ordered after the inflate that read it); every file reads
+    exactly as the host reader reads it."""
+    monkeypatch.setenv("MSW_GZ_NO_MAP", "0")
+    files = []
+    for k in range(5):
+        p = tmp_path / f"lane{k}.fastq.gz"
+        p.write_bytes(bgzf_compress(fastq_text(5_000 + 700 * k, 30 + k), 6))
+        files.append(str(p))
+    got = []
+    with GpuFastqReader(gpu_ctx, files[0], 256, 3000, with_pos=True, span_bytes=span) as g:
+        for k, f in enumerate(files):
+            if k:
+                g.reset(f)
+            if k + 1 < len(files):
+                g.prefetch(files[k + 1])
+            got.append(_drain(g))
+    for f, (gs, gl, gp) in zip(files, got):
+        hs, hl, hp, _ = host_reads(f)
+        assert np.array_equal(hl, gl) and np.array_equal(hp, gp) and np.array_equal(hs, gs), f
+
+
 @pytest.mark.parametrize("threads", ["3", "8"])
 def test_reader_parallel_compressed_reads(gpu_ctx, tmp_path, monkeypatch, threads):
     """Compressed top-ups split over several positioned-read threads
