@@ -421,24 +421,10 @@ void preupload_next(msw_gfastq* g) {
     msw_gfastq::Prefetch& p = g->pf;
     if (p.path.empty() || p.uploaded) return;
     join_prefetch(g);
-    if (!p.ok || !p.indexed || !p.used) return;
-    if (!g->us && hipStreamCreateWithFlags(&g->us, hipStreamNonBlocking) != hipSuccess) {
-        g->us = nullptr;
-        (void)hipGetLastError();
-        return;
-    }
-    if (!g->pre_up && (hipEventCreateWithFlags(&g->pre_up, hipEventDisableTiming) != hipSuccess ||
-                       hipEventCreateWithFlags(&g->pre_done, hipEventDisableTiming) != hipSuccess)) {
-        (void)hipGetLastError();
-        return;
-    }
+    if (!p.ok || !p.indexed || !p.used || !g->us || !g->pre_dc || p.used + kInPad > g->pre_dc_cap) return;
     if (g->pre_done_valid && hipStreamWaitEvent(g->us, g->pre_done, 0) != hipSuccess) {
         (void)hipGetLastError();
         return;
-    }
-    if (p.used + kInPad > g->pre_dc_cap) {
-        // a larger buffer: the previous one's readers finish first (hipFree waits)
-        if (grow(&g->pre_dc, &g->pre_dc_cap, p.used + kInPad)) return;
     }
     if (hipMemcpyAsync(g->pre_dc, p.map, p.used, hipMemcpyHostToDevice, g->us) != hipSuccess ||
         hipMemsetAsync(g->pre_dc + p.used, 0, kInPad, g->us) != hipSuccess ||
@@ -1003,6 +989,22 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
     drop_prefetch(g);
     const char* nm = getenv("MSW_GZ_NO_MAP");
     if (nm && atoi(nm) != 0) return MSW_OK;  // copied mode: nothing to pin ahead
+    if (!g->us) {
+        // the pre-upload's stream, events and buffer (preupload_next), made at
+        // the first prefetch -- a caller's setup -- not lazily at a file
+        // switch, where their creation stalled both workers' HIP calls
+        // ~25-30 ms; without them the reader uploads the span itself
+        (void)hipSetDevice(g->device);
+        if (hipStreamCreateWithFlags(&g->us, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&g->pre_up, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->pre_done, hipEventDisableTiming) != hipSuccess ||
+            grow(&g->pre_dc, &g->pre_dc_cap, g->in_cap + kInPad) != MSW_OK) {
+            (void)hipGetLastError();
+            if (g->pre_dc) (void)hipFree(g->pre_dc);
+            g->pre_dc = nullptr;
+            g->pre_dc_cap = 0;
+        }
+    }
     g->pf.path = path;
     const size_t cap = g->in_cap;
     const uint64_t span = g->span;
