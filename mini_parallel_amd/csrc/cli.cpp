@@ -762,6 +762,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
                 if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
                     die(std::string("GPU lane reader: ") + msw_last_error());
+                const double t_rd = ms_since(ts0);
                 const size_t kNone = ~(size_t)0;
                 size_t pending = kNone;
                 auto claim = [&]() -> size_t {
@@ -774,7 +775,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 // first window is ready when the clock starts
                 pending = claim();
                 if (pending != kNone) (void)msw_gfastq_prefetch(gr, st[pending]->path.c_str());
-                const double t_rd = ms_since(ts0);
                 const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
                 msw_genome* gen = nullptr;
                 const std::string& ref_seq = genome();

@@ -192,19 +192,14 @@ struct Inflater {
         h_flag = nullptr;
     }
     // upload cbytes of compressed data + the member table, inflate into out, check CRCs
-    // d_pre: the compressed bytes already on the device (cbytes + kInPad, the
-    // pad zeroed; the caller orders s after their upload), no upload here
     int run(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, uint8_t* out,
-            hipStream_t s, const uint8_t* d_pre = nullptr) {
+            hipStream_t s) {
         int rc;
+        if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
         if ((rc = grow(&d_mem, &mem_cap, mem.size()))) return rc;
         if ((rc = grow(&d_status, &status_cap, mem.size()))) return rc;
-        if (!d_pre) {
-            if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
-            if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
-            GZ_TRY(hipMemsetAsync(dc + cbytes, 0, kInPad, s));
-        }
-        const uint8_t* src = d_pre ? d_pre : dc;
+        if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
+        GZ_TRY(hipMemsetAsync(dc + cbytes, 0, kInPad, s));
         if (!mem.empty())
             GZ_TRY(hipMemcpyAsync(d_mem, mem.data(), mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
         GZ_TRY(hipMemsetAsync(d_flag, 0, 4, s));
@@ -222,7 +217,7 @@ struct Inflater {
         uint32_t* d_prof = nullptr;
         if (prof_on && n) GZ_TRY(hipMalloc((void**)&d_prof, (size_t)n * 64));
         if (d_prof) GZ_TRY(hipMemsetAsync(d_prof, 0, (size_t)n * 64, s));
-        GZ_TRY(msw::launch_gz_inflate(src, d_mem, n, out, d_status, d_flag, s, d_prof));
+        GZ_TRY(msw::launch_gz_inflate(dc, d_mem, n, out, d_status, d_flag, s, d_prof));
         if (timing) GZ_TRY(hipEventRecord(ev[1], s));
         if (d_prof) {
             std::vector<uint32_t> h((size_t)n * 16);
@@ -321,19 +316,8 @@ struct msw_gfastq {
         size_t used = 0;
         uint64_t obytes = 0;
         bool indexed = false;
-        bool uploaded = false;  // that span copied to pre_dc (preupload_next)
         std::thread th;
     } pf;
-    // The prefetched file's first span on the device: copied on stream us at
-    // this file's last span (preupload_next), so the next file's first
-    // inflate does not wait on PCIe; pre_done orders the next copy after the
-    // inflate that read it
-    uint8_t* pre_dc = nullptr;
-    size_t pre_dc_cap = 0;
-    hipStream_t us = nullptr;
-    hipEvent_t pre_up = nullptr, pre_done = nullptr;
-    bool pre_done_valid = false;
-    bool pre_uploaded = false;  // the adopted file's first span is in pre_dc
     // a prefetched file's first span, indexed ahead (open_file adopts it)
     std::vector<msw::GzMember> pre_mem;
     size_t pre_used = 0;
@@ -399,7 +383,6 @@ void join_prefetch(msw_gfastq* g) {
 void drop_prefetch(msw_gfastq* g) {
     join_prefetch(g);
     msw_gfastq::Prefetch& p = g->pf;
-    if (p.uploaded && g->us) (void)hipStreamSynchronize(g->us);  // the copy reads the pinned window
     if (p.reg_len) (void)hipHostUnregister(p.map);
     if (p.map) munmap(p.map, (size_t)p.fsize);
     if (p.f) fclose(p.f);
@@ -408,48 +391,17 @@ void drop_prefetch(msw_gfastq* g) {
     p.fsize = p.reg_len = 0;
     p.ok = false;
     p.indexed = false;
-    p.uploaded = false;
     p.mem.clear();
     p.path.clear();
-}
-
-// At this file's last span (its own upload done): the prefetched next file's
-// first span -- pinned and indexed on the prefetch thread -- goes to the
-// device on stream us, beside this span's inflate, parse and scoring.  Any
-// failure leaves it to next_span's own upload.
-void preupload_next(msw_gfastq* g) {
-    msw_gfastq::Prefetch& p = g->pf;
-    if (p.path.empty() || p.uploaded) return;
-    join_prefetch(g);
-    if (!p.ok || !p.indexed || !p.used || !g->us || !g->pre_dc || p.used + kInPad > g->pre_dc_cap) return;
-    if (g->pre_done_valid && hipStreamWaitEvent(g->us, g->pre_done, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        return;
-    }
-    if (hipMemcpyAsync(g->pre_dc, p.map, p.used, hipMemcpyHostToDevice, g->us) != hipSuccess ||
-        hipMemsetAsync(g->pre_dc + p.used, 0, kInPad, g->us) != hipSuccess ||
-        hipEventRecord(g->pre_up, g->us) != hipSuccess) {
-        (void)hipGetLastError();
-        (void)hipStreamSynchronize(g->us);
-        return;
-    }
-    p.uploaded = true;
 }
 
 void unmap_file(msw_gfastq* g);
 
 void release(msw_gfastq* g) {
     join_filler(g);
-    (void)hipSetDevice(g->device);
     drop_prefetch(g);
+    (void)hipSetDevice(g->device);
     if (g->rs) (void)hipStreamSynchronize(g->rs);
-    if (g->us) {
-        (void)hipStreamSynchronize(g->us);
-        (void)hipStreamDestroy(g->us);
-    }
-    if (g->pre_up) (void)hipEventDestroy(g->pre_up);
-    if (g->pre_done) (void)hipEventDestroy(g->pre_done);
-    if (g->pre_dc) (void)hipFree(g->pre_dc);
     unmap_file(g);
     if (g->f) fclose(g->f);
     for (int i = 0; i < 2; ++i) {
@@ -680,14 +632,7 @@ int next_span(msw_gfastq* g) {
     const size_t lead = g->mapped ? (size_t)(g->map_off - g->reg_lo) : 0;
     if (lead)
         for (msw::GzMember& m : g->mem) m.coff += lead;
-    const bool pre = g->pre_uploaded;  // a prefetched first span already on the device
-    g->pre_uploaded = false;
-    if (pre) GZ_TRY(hipStreamWaitEvent(s, g->pre_up, 0));
-    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s, pre ? g->pre_dc : nullptr))) return rc;
-    if (pre) {
-        GZ_TRY(hipEventRecord(g->pre_done, s));
-        g->pre_done_valid = true;
-    }
+    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s))) return rc;
     // 3. the previous span's unfinished line goes right in front
     const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
     if (carry > kCarry)
@@ -720,7 +665,6 @@ int next_span(msw_gfastq* g) {
     if (lead)  // uploads done: the member table holds offsets into hc again
         for (msw::GzMember& m : g->mem) m.coff -= lead;
     if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
-    if (last) preupload_next(g);
     // the upload of hc has completed: drop the consumed bytes and read ahead
     if (g->mapped) {
         // the window's upload is done: unpin it; the next one registers in the background
@@ -798,11 +742,9 @@ int open_file(msw_gfastq* g, const char* path) {
     join_filler(g);
     join_prefetch(g);
     if (g->mapped || g->map) {
-        // the previous file's last window may still be uploading (and its
-        // first span's pre-upload, when it was never read)
+        // the previous file's last window may still be uploading
         GZ_TRY(hipSetDevice(g->device));
         GZ_TRY(hipStreamSynchronize(g->rs));
-        if (g->us) GZ_TRY(hipStreamSynchronize(g->us));
         unmap_file(g);
     }
     if (g->f) fclose(g->f);
@@ -822,7 +764,7 @@ int open_file(msw_gfastq* g, const char* path) {
     g->fill_rc = 0;
     g->last_used = 0;
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
-    g->pre_indexed = g->pre_uploaded = false;
+    g->pre_indexed = false;
     if (g->pf.ok && g->pf.path == path) {
         // prefetched (msw_gfastq_prefetch): file open, mapped, first window
         // [0, reg_len) pinned -- the state register_window leaves behind
@@ -841,14 +783,12 @@ int open_file(msw_gfastq* g, const char* path) {
             g->pre_used = p.used;
             g->pre_obytes = p.obytes;
             g->pre_indexed = true;
-            g->pre_uploaded = p.uploaded;
         }
         p.f = nullptr;
         p.map = nullptr;
         p.fsize = p.reg_len = 0;
         p.ok = false;
         p.indexed = false;
-        p.uploaded = false;
         p.mem.clear();
         p.path.clear();
         if (g->d_state) {
@@ -989,22 +929,6 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
     drop_prefetch(g);
     const char* nm = getenv("MSW_GZ_NO_MAP");
     if (nm && atoi(nm) != 0) return MSW_OK;  // copied mode: nothing to pin ahead
-    if (!g->us) {
-        // the pre-upload's stream, events and buffer (preupload_next), made at
-        // the first prefetch -- a caller's setup -- not lazily at a file
-        // switch, where their creation stalled both workers' HIP calls
-        // ~25-30 ms; without them the reader uploads the span itself
-        (void)hipSetDevice(g->device);
-        if (hipStreamCreateWithFlags(&g->us, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&g->pre_up, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&g->pre_done, hipEventDisableTiming) != hipSuccess ||
-            grow(&g->pre_dc, &g->pre_dc_cap, g->in_cap + kInPad) != MSW_OK) {
-            (void)hipGetLastError();
-            if (g->pre_dc) (void)hipFree(g->pre_dc);
-            g->pre_dc = nullptr;
-            g->pre_dc_cap = 0;
-        }
-    }
     g->pf.path = path;
     const size_t cap = g->in_cap;
     const uint64_t span = g->span;

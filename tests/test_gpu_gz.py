@@ -275,10 +275,9 @@ def test_reader_prefetch_next_file(gpu_ctx, tmp_path, monkeypatch, mode):
 @pytest.mark.parametrize("span", [1 << 20, 1 << 18])
 def test_reader_prefetch_chain(gpu_ctx, tmp_path, monkeypatch, span):
     """Lane files read back to back, each with the next one prefetched (the
-    --full-wgs worker's order): at a file's last span the next file's first
-    span is copied to the device ahead (one buffer, reused file after file,
-    its reuse ordered after the inflate that read it); every file reads
-    exactly as the host reader reads it."""
+    --full-wgs worker's order: reset, then prefetch the file after it), so
+    every file after the first is adopted with its first span indexed on the
+    prefetch thread; every file reads exactly as the host reader reads it."""
     monkeypatch.setenv("MSW_GZ_NO_MAP", "0")
     files = []
     for k in range(5):
