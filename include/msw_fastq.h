@@ -104,8 +104,9 @@ int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out);
  * batches may still be running while the new file is inflated and parsed. */
 int msw_gfastq_reset(msw_gfastq* g, const char* path);
 /* Name the lane file the next msw_gfastq_reset will open: it is opened,
- * mapped and its first window of compressed bytes pinned by a host thread
- * now, beside the current file's spans, so the reset adopts it instead of
+ * mapped, its first window of compressed bytes pinned and that window's
+ * first span of BGZF members indexed by a host thread now, beside the
+ * current file's spans, so the reset adopts it instead of
  * waiting for it (a new file's first window cost ~18-25 ms against 2-4 ms
  * for later ones: tools/gfastq_trace_c4.sh).  Optional; a reset to another
  * path opens that path as usual, and failures here only leave the reset to
