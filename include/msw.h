@@ -97,9 +97,8 @@ int msw_device_count(int* n);
 int msw_device_info(int ordinal, msw_device_info_t* out);
 
 /* gpu.rs:97-132 get_opencl_context/init_opencl: one context per device with
- * a compute stream (its copy, readback, second compute and long-pair streams
- * are made on first use) and three pinned staging slots (up to three chunks
- * in flight). */
+ * compute, copy and readback streams and three pinned staging slots (up to
+ * three chunks in flight). */
 int msw_ctx_create(int ordinal, msw_ctx** out);
 void msw_ctx_destroy(msw_ctx* ctx);
 

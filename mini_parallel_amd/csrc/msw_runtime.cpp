@@ -267,7 +267,6 @@ void free_slot(Slot& s) {
 struct msw_ctx {
     int device = 0;
     int cu_count = 256;
-    // compute is made with the context, the others on first use (ensure_stream)
     hipStream_t compute = nullptr, copy = nullptr, d2h = nullptr;
     // multi-chunk calls alternate their chunks' kernels over compute and
     // compute2, so chunk k+1's waves start under chunk k's tail (one stream
@@ -679,17 +678,7 @@ struct SideFork {
     }
 };
 
-// The context's streams besides compute are made on first use: a context
-// that only scores device batches (the --full-wgs GPU reader's workers) never
-// pays their creation (2-35 ms each on a fresh box, tools/setup_probe.cpp).
-int ensure_stream(hipStream_t* s) {
-    if (!*s) HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-    return MSW_OK;
-}
-
 int fork_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
-    int rc = ensure_stream(&ctx->side);
-    if (rc) return rc;
     HIP_TRY(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(f.ev, st));
     HIP_TRY(hipStreamWaitEvent(ctx->side, f.ev, 0));
@@ -956,8 +945,6 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     // alternate that stream, so consecutive calls still overlap.
     const bool multi_chunk = n > chunk;
     const bool alternate = multi_chunk || !sync;
-    if (alternate && (rc = ensure_stream(&ctx->compute2))) return rc;
-    if (multi_chunk && ((rc = ensure_stream(&ctx->copy)) || (rc = ensure_stream(&ctx->d2h)))) return rc;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
@@ -1096,8 +1083,11 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     for (Slot& s : ctx->slots) dropped = dropped || (s.busy && s.ticket == ticket);
     if (dropped) {
         const std::string msg = g_last_error;
-        for (hipStream_t q : {ctx->copy, ctx->compute, ctx->compute2, ctx->d2h, ctx->side})
-            if (q) (void)hipStreamSynchronize(q);
+        (void)hipStreamSynchronize(ctx->copy);
+        (void)hipStreamSynchronize(ctx->compute);
+        (void)hipStreamSynchronize(ctx->compute2);
+        (void)hipStreamSynchronize(ctx->d2h);
+        (void)hipStreamSynchronize(ctx->side);
         for (Slot& s : ctx->slots)
             if (s.busy && s.ticket == ticket) s.busy = false;
         ctx->next_ticket++;
@@ -1189,6 +1179,10 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
     if (e == hipSuccess && hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->epoch);
     if (e == hipSuccess) e = hipEventRecord(c->epoch, c->compute);
     if (e != hipSuccess) {
@@ -1586,10 +1580,9 @@ int msw_genome_create(msw_ctx* ctx, const uint8_t* seq, uint64_t len, msw_genome
         delete g;
         return fail(MSW_E_NOMEM, "hipMalloc(%llu B) for the genome: %s", (unsigned long long)len, hipGetErrorString(e));
     }
-    // synchronous: on the compute stream (the other streams are made on first use)
-    e = hipMemsetAsync(g->d_seq + len, 0, msw::kGenomePad, ctx->compute);
-    if (e == hipSuccess && len) e = hipMemcpyAsync(g->d_seq, seq, len, hipMemcpyHostToDevice, ctx->compute);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->compute);
+    e = hipMemsetAsync(g->d_seq + len, 0, msw::kGenomePad, ctx->copy);
+    if (e == hipSuccess && len) e = hipMemcpyAsync(g->d_seq, seq, len, hipMemcpyHostToDevice, ctx->copy);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->copy);
     if (e != hipSuccess) {
         msw_genome_destroy(g);
         return fail(MSW_E_DEVICE, "genome upload: %s", hipGetErrorString(e));
@@ -1775,8 +1768,9 @@ int msw_synchronize(msw_ctx* ctx) {
     int rc = set_device(ctx);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->compute));
-    for (hipStream_t q : {ctx->compute2, ctx->copy, ctx->d2h, ctx->side})
-        if (q) HIP_TRY(hipStreamSynchronize(q));
+    HIP_TRY(hipStreamSynchronize(ctx->compute2));
+    HIP_TRY(hipStreamSynchronize(ctx->copy));
+    HIP_TRY(hipStreamSynchronize(ctx->d2h));
     HIP_TRY(hipGetLastError());
     return MSW_OK;
 }
