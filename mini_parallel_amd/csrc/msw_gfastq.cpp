@@ -878,7 +878,23 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     if (hipSetDevice(g->device) != hipSuccess) return bail(set_error(MSW_E_DEVICE, "hipSetDevice failed"));
     int rc;
     if ((rc = g->inf.init())) return bail(rc);
-    if (hipStreamCreateWithFlags(&g->rs, hipStreamNonBlocking) != hipSuccess ||
+    // The reader's stream gets a hardware queue of its own: a stream with a
+    // CU mask (here all CUs) is not placed on one of the GPU_MAX_HW_QUEUES
+    // queues that plain streams share, where the --full-wgs traces showed one
+    // worker's inflate and parse kernels queued with a scoring stream
+    // (DESIGN.md 6.2).  A plain stream if the masked one cannot be made.
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        std::vector<uint32_t> mask(((size_t)ncu + 31) / 32, 0xFFFFFFFFu);
+        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+        if (hipExtStreamCreateWithCUMask(&g->rs, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
+            g->rs = nullptr;
+        }
+    }
+    if ((!g->rs && hipStreamCreateWithFlags(&g->rs, hipStreamNonBlocking) != hipSuccess) ||
         hipEventCreateWithFlags(&g->parsed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&g->emitted[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&g->emitted[1], hipEventDisableTiming) != hipSuccess)
