@@ -89,7 +89,10 @@ int msw_is_bgzf(const char* path);
  * its page-cache pages are mapped (MAP_SHARED) and DMA'd in place.  A file
  * found shorter than when it was opened is reported (MSW_E_INVALID) at the
  * next span; one truncated while a span's member headers are being indexed
- * can raise SIGBUS.  MSW_GZ_NO_MAP=1 reads through pread copies instead. */
+ * can raise SIGBUS.  MSW_GZ_NO_MAP=1 reads through pread copies instead.
+ * The reader inflates and parses on a stream of its own, made with a CU mask
+ * (all CUs) so that it has a hardware queue of its own; such a stream is
+ * ordered with work on the null stream. */
 int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64_t max_reads, int want_pos,
                     uint64_t span_bytes, msw_gfastq** out);
 /* The next batch, enqueued on `stream` (a hipStream_t; NULL = the context's
