@@ -509,8 +509,7 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
         for (uint32_t G = 16; G >= 8; --G) {
             if (force_g ? G != force_g : ((force_pairs || force_split) && G != 16)) continue;
             const int kr = msw::rows_per_lane(max_m, split, G);
-            // KR 17..24 (reads of 257..384 bases) only in 16-lane groups
-            if (kr > (split ? 8 : (G == 16 ? msw::kMaxRowsPerLane : 16))) continue;
+            if (kr > (split ? 8 : msw::kMaxRowsPerLane)) continue;
             const uint32_t groups = 64 / G;
             if (G != 16 && msw::lds_bytes(stride, groups) > 65536) continue;
             const uint64_t per = msw::pairs_per_wave(split, groups);
