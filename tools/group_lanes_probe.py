@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Lanes per pair group for large batches of 150 bp reads x 300 bp windows:
 the layout model's choice (G = 8, KR = 19 once 17..24 packed rows are
-allowed for any G) against 16-lane groups (KR = 10) and 10 / 12-lane groups,
-forced with MSW_GROUP_LANES.  Device-resident batches, HIP events over R
-launches after a preheat; scores (and coordinates) must agree across G.
+allowed for any G) against 16-lane groups (KR = 10),
+forced with MSW_GROUP_LANES, alternating three times (the clock drifts over
+seconds of load, so a fixed order biases later settings).  Device-resident
+batches, HIP events over R launches after a preheat; scores (and
+coordinates) must agree across G.
 
   python3 tools/group_lanes_probe.py [--reps 20]
 """
@@ -31,13 +33,13 @@ def main():
     ctx = Context(0)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    for n in (65536, 1 << 20):
+    for n in (65536, 131072, 262144, 1 << 20):
         b = config_shard(3, 0, n)  # 150 bp reads (indels: 149-151) x 300 bp windows
         t = lambda x, dt=None: torch.from_numpy(np.ascontiguousarray(x if dt is None else x.view(dt))).to(dev)  # noqa
         r, w, rl, wl = t(b.reads), t(b.wins), t(b.read_len, np.int16), t(b.win_len, np.int16)
         for name, sc in (("linear", LINEAR), ("linear_coords", LINEAR_COORDS), ("affine_coords", AFFINE)):
             ref = None
-            for g in ("auto", "16", "12", "10", "8"):
+            for g in ("auto", "16", "auto", "16", "auto", "16"):  # alternating: clocks drift under load
                 if g == "auto":
                     os.environ.pop("MSW_GROUP_LANES", None)
                 else:
