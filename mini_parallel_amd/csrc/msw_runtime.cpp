@@ -516,10 +516,11 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
             // 17..24 rows in narrower groups (150 bp reads: G = 8, KR = 19, 152
             // rows, no idle lane) fit only 3-4 waves per SIMD (122 VGPRs, the
             // LDS of 8 window streams), which the model does not see: only for
-            // batches of >= 8 waves per SIMD, where it measured 5-6 % faster
-            // than G = 16 (1M pairs); at 65k pairs it was 18 % slower
+            // batches of >= 48 waves per SIMD.  Measured against G = 16 at 1M
+            // pairs 5-6 % faster (linear, linear + cell, affine + cell); at
+            // 262k 4 % faster to 13 % slower, at 65k up to 18 % slower
             // (tools/group_lanes_probe.py)
-            if (!split && G != 16 && kr > 16 && !force_g && (n_pairs + per - 1) / per < 8 * simds) continue;
+            if (!split && G != 16 && kr > 16 && !force_g && (n_pairs + per - 1) / per < 48 * simds) continue;
             const double t = makespan((n_pairs + per - 1) / per, wave_instr(split, G), 0, 0.0);
             if (t < best_t * 0.995) {
                 best_t = t;
