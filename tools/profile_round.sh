@@ -1,6 +1,6 @@
 #!/bin/bash
 # Collect the round's rocprofv3 evidence for the bench workloads (run on the GPU
-# box from the repo root):  bash tools/profile_round.sh r01
+# box from the repo root):  bash tools/profile_round.sh r01   [CONFIGS="3" for one]
 # Per config: one kernel-trace pass (--stats), then one PMC pass per counter
 # group (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950; see
 # MI355X_MICROARCH.md "rocprofv3 PMC slots").  The bench runs without the CPU
@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 # the commit of the profiled tree (the GPU box has no .git: pass it in)
 echo "${MSW_COMMIT:-unknown}" > "$OUT/COMMIT"
 export TMPDIR=/tmp
-for CFG in 2 3 5; do
+for CFG in ${CONFIGS:-2 3 5}; do  # CONFIGS="3": one config only
   case $CFG in
     2) ARGS="--steps 50 --warmup 5" ;;
     3) ARGS="--steps 5 --warmup 2" ;;

@@ -2,7 +2,9 @@
 """Summarise tools/profile_round.sh output into profiles/<round>/ and
 profiles/pmc_traffic.json (per-launch HBM bytes for bench.py's roofline,
 keyed "config<k>:<kind>" as bench.py looks them up).
-Usage: python tools/summarize_profile.py r01"""
+Usage: python tools/summarize_profile.py r01 [--only 3]
+(--only: refresh those configs' entries and keep the others, e.g. config 2's
+hand-split non-sequence fetch)"""
 import csv
 import glob
 import json
@@ -26,6 +28,7 @@ def counters(path):
 
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    only = {int(x) for x in sys.argv[sys.argv.index("--only") + 1].split(",")} if "--only" in sys.argv else None
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
@@ -39,6 +42,8 @@ def main():
         commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
                                 text=True).stdout.strip()
     for cfg in (2, 3, 5):
+        if only and cfg not in only:
+            continue
         d = os.path.join(src, f"c{cfg}")
         if not os.path.isdir(d):
             continue
@@ -64,9 +69,14 @@ def main():
                     "note": "FETCH_SIZE x 2 (gfx950 reports half of wide 16 B/lane reads, "
                             "MI355X_MICROARCH.md HBM section) + WRITE_SIZE; per launch; the batch is "
                             "re-read every step and may be served from the 256 MiB Infinity Cache"}
-    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if only:  # merge: the other configs' entries stay as they are
+        old = json.load(open(tpath)) if os.path.exists(tpath) else {}
+        old.update(traffic)
+        traffic = old
+    with open(os.path.join(dst, "pmc_summary.json" if not only else "pmc_summary_only.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
+    with open(tpath, "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic, indent=1))
 
