@@ -46,7 +46,9 @@ def layout(request, monkeypatch):
     from a makespan model ("auto"; mixed-length batches then run as one
     length-bucketed sw_multi_kernel launch); a forced layout launches each
     length bucket on its own, and a forced G that cannot hold the batch's reads
-    (KR > 16, or the LDS budget) falls back to G = 16."""
+    (KR > 24, or the LDS budget) falls back to G = 16.  Forced G = 8 / 9 on
+    the 150 bp batches runs 19 / 17 packed rows per lane, the narrow groups
+    the model picks for batches of >= 48 waves per SIMD."""
     if request.param == "auto":
         for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
             monkeypatch.delenv(k, raising=False)
