@@ -16,7 +16,7 @@ constexpr uint32_t kWinSentinel2 = 0x40004000u;
 
 constexpr int kGroupLanes = 16;        // one DPP row
 constexpr int kPairsPerWave = 8;       // 4 groups x 2 packed pairs
-constexpr int kMaxRowsPerLane = 24;    // pairs layout: KR <= 16 for any G, 17..24 with G = 16
+constexpr int kMaxRowsPerLane = 24;    // pairs layout, any G (17..24 in narrow groups: large batches only)
 constexpr int kMaxMultiKR = 16;        // sw_multi_kernel's rows-per-lane range
 constexpr int kMaxReadLen = 384;       // 16 x 24
 constexpr int kMaxWinLen = 4096;
