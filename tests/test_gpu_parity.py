@@ -109,6 +109,22 @@ def test_config3_affine_coords_sample(gpu_ctx, layout, oracle):
     assert_same(gpu_run(gpu_ctx, b, sc, chunk=9_000), oracle_run(oracle, b, sc), True)
 
 
+@pytest.mark.parametrize("sc", [Scoring(), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)],
+                         ids=["linear", "affine_coords"])
+def test_narrow_groups_large_batch(gpu_ctx, oracle, monkeypatch, sc):
+    """A batch large enough (>= 48 waves per SIMD) that the layout model
+    takes narrow lane groups of 17..24 rows (150 bp reads: G = 8 or 9) on its
+    own, as one launch: every pair against the SIMD oracle."""
+    for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
+        monkeypatch.delenv(k, raising=False)
+    b = config_batch(3, n_pairs=800_000)
+    got = gpu_run(gpu_ctx, b, sc, chunk=800_000)
+    s, i, j, _ = oracle.sw_batch_simd(b.reads, b.read_len, b.wins, b.win_len, match=sc.match, mismatch=sc.mismatch,
+                                      gap_open=sc.gap_open, gap_extend=sc.gap_extend, affine=sc.affine,
+                                      threads=THREADS, coords=sc.want_coords)
+    assert_same(got, (s, i, j), sc.want_coords)
+
+
 def test_config5_mixed_lengths(gpu_ctx, layout, oracle):
     """Config 5 shape: 75-250 bp reads, window 2m, length-bucketed dispatch."""
     b = config_batch(5, n_pairs=12_000)
