@@ -211,9 +211,12 @@ msw::SwParams base_params(const Scheme& s) {
 }
 
 // Device + pinned buffers for one in-flight chunk.  The per-pair metadata of a
-// chunk (window positions, slot order, read and window lengths) is one block,
-// [pos i64 | order u32 | rlen u16 | wlen u16] x cap_pairs, uploaded by ONE
-// copy; the results [score i32 | end_i i16 | end_j i16] come back by one.
+// chunk (window positions, read and window lengths, slot order) is one block,
+// [pos i64 | rlen u16 | wlen u16 | order u32] x n, uploaded by ONE copy of the
+// part the chunk uses (pairs mode skips the positions, a chunk in input order
+// the order); the results [score i32 | end_i i16 | end_j i16] come back by one
+// copy, or are written by the kernels straight into the pinned block (a
+// one-chunk call: no copy and no event between the kernel and the host).
 struct Slot {
     size_t cap_pairs = 0, cap_read = 0, cap_win = 0;
     uint8_t *d_reads = nullptr, *d_wins = nullptr, *d_meta = nullptr, *d_res = nullptr;
@@ -224,17 +227,24 @@ struct Slot {
     uint16_t *d_rlen = nullptr, *d_wlen = nullptr, *h_rlen = nullptr, *h_wlen = nullptr;
     int32_t *d_score = nullptr, *h_score = nullptr;
     int16_t *d_ei = nullptr, *d_ej = nullptr, *h_ei = nullptr, *h_ej = nullptr;
+    // where this chunk's kernels store results: the device block or the host one
+    int32_t* k_score = nullptr;
+    int16_t *k_ei = nullptr, *k_ej = nullptr;
     hipEvent_t uploaded = nullptr, computed = nullptr, done = nullptr;
-    hipEvent_t k_start = nullptr, k_end = nullptr;  // timing events around the chunk's scoring launch
+    // timing events around the chunk's scoring launches; a chunk whose kernels
+    // write the host block directly ends on k_end (done is not recorded)
+    hipEvent_t k_start = nullptr, k_end = nullptr;
     bool busy = false;
     bool by_slot = false;  // results in slot order: the drain scatters them through h_order
+    bool direct_out = false;  // the kernels wrote h_res themselves; k_end marks completion
     uint64_t ticket = 0;  // msw_align_*_async call that owns the chunk in flight
+    uint64_t seq = 0;     // submission order of the chunk (drains go in this order)
     // Pending readback bookkeeping.
     uint64_t first = 0, count = 0;
     msw_out_t out{};
 };
 
-constexpr size_t kMetaBytesPerPair = 8 + 4 + 2 + 2;
+constexpr size_t kMetaBytesPerPair = 8 + 2 + 2 + 4;
 constexpr size_t kResBytesPerPair = 4 + 2 + 2;
 
 // Views of the metadata / result blocks for a chunk of n pairs (each array
@@ -243,9 +253,9 @@ void set_views(Slot& s, uint64_t n) {
     auto views = [n](uint8_t* meta, uint8_t* res, int64_t*& pos, uint32_t*& order, uint16_t*& rlen, uint16_t*& wlen,
                      int32_t*& score, int16_t*& ei, int16_t*& ej) {
         pos = reinterpret_cast<int64_t*>(meta);
-        order = reinterpret_cast<uint32_t*>(meta + 8 * n);
-        rlen = reinterpret_cast<uint16_t*>(meta + 12 * n);
-        wlen = reinterpret_cast<uint16_t*>(meta + 14 * n);
+        rlen = reinterpret_cast<uint16_t*>(meta + 8 * n);
+        wlen = reinterpret_cast<uint16_t*>(meta + 10 * n);
+        order = reinterpret_cast<uint32_t*>(meta + 12 * n);
         score = reinterpret_cast<int32_t*>(res);
         ei = reinterpret_cast<int16_t*>(res + 4 * n);
         ej = reinterpret_cast<int16_t*>(res + 6 * n);
@@ -281,8 +291,19 @@ struct msw_ctx {
     uint64_t next_ticket = 1, done_ticket = 0;
     uint64_t slot_seq = 0;  // chunks submitted (slot = slot_seq % kSlots)
     msw_stats_t stats{};    // msw_ctx_stats: host-batch calls since creation / the last reset
-    hipEvent_t epoch = nullptr;  // recorded at creation: the origin of kernel_busy's interval union
+    // Origin of the kernel-time interval union (recorded at creation, moved
+    // forward every ~second of GPU time so float ms offsets stay fine-grained:
+    // epoch_next is recorded, and once it has completed becomes the epoch)
+    hipEvent_t epoch = nullptr, epoch_next = nullptr;
     double busy_until = 0.0;     // ms after epoch at which the counted scoring intervals end
+    // pinned_cached: the last few (address, bytes) ranges asked about
+    struct PinnedRange {
+        const void* p = nullptr;
+        size_t bytes = 0;
+        bool pinned = false;
+    };
+    PinnedRange pinned_ranges[4];
+    unsigned pinned_next = 0;
     // compat buffers
     uint8_t *c_s1 = nullptr, *c_s2 = nullptr;
     int32_t* c_res = nullptr;
@@ -342,6 +363,9 @@ hipEvent_t take_event(msw_ctx* ctx) {
 // offsets against the context's epoch event.  Intervals arrive in
 // submission order, i.e. in start order but for a chunk that starts before
 // its predecessor, which is then undercounted, never counted twice.
+// Callers hand intervals over oldest chunk first (drain_through), so each
+// starts no earlier than the previous one save for the two compute streams'
+// overlap, which is exactly what the union removes.
 void add_kernel_interval(msw_ctx* ctx, hipEvent_t k0, hipEvent_t k1) {
     float dur = 0.f, start = 0.f;
     if (hipEventElapsedTime(&dur, k0, k1) != hipSuccess) {
@@ -356,6 +380,29 @@ void add_kernel_interval(msw_ctx* ctx, hipEvent_t k0, hipEvent_t k1) {
     const double covered = std::min<double>(dur, std::max(0.0, ctx->busy_until - start));
     ctx->stats.kernel_ms += dur - covered;
     ctx->busy_until = std::max<double>(ctx->busy_until, (double)start + dur);
+    // Re-base: a float offset of T ms resolves T / 2^24 -- 0.25 ms after an
+    // hour -- so the epoch moves up once it is a second behind.  The new one
+    // is an event on the compute stream; it takes over once it has completed
+    // and its distance from the old one is known (both offsets then move by
+    // it; an interval starting before it gets a negative offset, which the
+    // union handles the same way).
+    if (ctx->epoch_next) {
+        float delta = 0.f;
+        if (hipEventQuery(ctx->epoch_next) == hipSuccess &&
+            hipEventElapsedTime(&delta, ctx->epoch, ctx->epoch_next) == hipSuccess) {
+            ctx->busy_until -= delta;
+            std::swap(ctx->epoch, ctx->epoch_next);
+            (void)hipEventDestroy(ctx->epoch_next);
+            ctx->epoch_next = nullptr;
+        }
+        (void)hipGetLastError();
+    } else if (start > 1000.f) {
+        if (hipEventCreate(&ctx->epoch_next) != hipSuccess || hipEventRecord(ctx->epoch_next, ctx->compute) != hipSuccess) {
+            if (ctx->epoch_next) (void)hipEventDestroy(ctx->epoch_next);
+            ctx->epoch_next = nullptr;
+            (void)hipGetLastError();
+        }
+    }
 }
 
 // Kernel time of finished msw_align_reads_device launches into ctx->stats
@@ -384,11 +431,11 @@ int grow_dev(T** p, size_t n) {
     return MSW_OK;
 }
 template <typename T>
-int grow_host(T** p, size_t n) {
+int grow_host(T** p, size_t n, unsigned flags = hipHostMallocDefault) {
     if (*p) (void)hipHostFree(*p);
     *p = nullptr;
     if (n == 0) return MSW_OK;
-    hipError_t e = hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc((void**)p, n * sizeof(T), flags);
     if (e != hipSuccess) return fail(MSW_E_NOMEM, "hipHostMalloc(%zu B): %s", n * sizeof(T), hipGetErrorString(e));
     return MSW_OK;
 }
@@ -403,9 +450,12 @@ int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
         HIP_TRY(hipEventCreate(&s.k_end));
     }
     if (pairs > s.cap_pairs) {
+        // the result block is mapped and coherent: one-chunk calls have the
+        // kernels store into it directly (its device address is the host one)
         if ((rc = grow_dev(&s.d_meta, pairs * kMetaBytesPerPair)) ||
             (rc = grow_host(&s.h_meta, pairs * kMetaBytesPerPair)) ||
-            (rc = grow_dev(&s.d_res, pairs * kResBytesPerPair)) || (rc = grow_host(&s.h_res, pairs * kResBytesPerPair)))
+            (rc = grow_dev(&s.d_res, pairs * kResBytesPerPair)) ||
+            (rc = grow_host(&s.h_res, pairs * kResBytesPerPair, hipHostMallocMapped | hipHostMallocCoherent)))
             return rc;
         s.cap_pairs = pairs;
     }
@@ -717,9 +767,9 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.out_by_slot = use_order ? 1u : 0u;
         p.out_slot_base = b.begin;
         p.slot_base = use_order ? 0u : b.begin;
-        p.score = s.d_score;
-        p.end_i = sch.coords ? s.d_ei : nullptr;
-        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.score = s.k_score;
+        p.end_i = sch.coords ? s.k_ei : nullptr;
+        p.end_j = sch.coords ? s.k_ej : nullptr;
         p.read_stride = read_stride;
         p.win_stride = win_stride;
         int rc = n_short ? fork_side(ctx, cs, side) : MSW_OK;
@@ -738,9 +788,9 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.read_len = s.d_rlen;
         p.win_len = s.d_wlen;
         p.order = s.d_order;
-        p.score = s.d_score;
-        p.end_i = sch.coords ? s.d_ei : nullptr;
-        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.score = s.k_score;
+        p.end_i = sch.coords ? s.k_ei : nullptr;
+        p.end_j = sch.coords ? s.k_ej : nullptr;
         p.read_stride = read_stride;
         p.win_stride = win_stride;
         p.win_vec = msw::vec_ok(p.wins, p.win_stride);
@@ -763,9 +813,9 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.read_len = s.d_rlen;
         p.win_len = s.d_wlen;
         p.order = s.d_order;
-        p.score = s.d_score;
-        p.end_i = sch.coords ? s.d_ei : nullptr;
-        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.score = s.k_score;
+        p.end_i = sch.coords ? s.k_ei : nullptr;
+        p.end_j = sch.coords ? s.k_ej : nullptr;
         p.read_stride = read_stride;
         p.win_stride = win_stride;
         p.win_vec = msw::vec_ok(p.wins, p.win_stride);
@@ -788,9 +838,9 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.order = use_order ? s.d_order + b.begin : nullptr;
         p.out_by_slot = use_order ? 1u : 0u;
         p.out_slot_base = b.begin;
-        p.score = s.d_score;
-        p.end_i = sch.coords ? s.d_ei : nullptr;
-        p.end_j = sch.coords ? s.d_ej : nullptr;
+        p.score = s.k_score;
+        p.end_i = sch.coords ? s.k_ei : nullptr;
+        p.end_j = sch.coords ? s.k_ej : nullptr;
         p.read_stride = read_stride;
         p.win_stride = win_stride;
         p.n_slots = b.count;
@@ -813,7 +863,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
 int drain_slot(msw_ctx* ctx, Slot& s) {
     if (!s.busy) return MSW_OK;
     s.busy = false;
-    HIP_TRY(hipEventSynchronize(s.done));
+    HIP_TRY(hipEventSynchronize(s.direct_out ? s.k_end : s.done));
     add_kernel_interval(ctx, s.k_start, s.k_end);
     if (s.by_slot) {  // length-bucketed chunk: slot k holds pair h_order[k]
         int32_t* sc = s.out.score + s.first;
@@ -831,6 +881,19 @@ int drain_slot(msw_ctx* ctx, Slot& s) {
     if (s.out.end_i) memcpy(s.out.end_i + s.first, s.h_ei, s.count * sizeof(int16_t));
     if (s.out.end_j) memcpy(s.out.end_j + s.first, s.h_ej, s.count * sizeof(int16_t));
     return MSW_OK;
+}
+
+// Drain the busy slots whose ticket is <= `ticket` (all: UINT64_MAX) oldest
+// chunk first, so the kernel-time union sees its intervals in start order.
+int drain_through(msw_ctx* ctx, uint64_t ticket) {
+    for (;;) {
+        Slot* next = nullptr;
+        for (Slot& s : ctx->slots)
+            if (s.busy && s.ticket <= ticket && (!next || s.seq < next->seq)) next = &s;
+        if (!next) return MSW_OK;
+        const int rc = drain_slot(ctx, *next);
+        if (rc) return rc;
+    }
 }
 
 int validate_batch(const msw_batch_t* b, const msw_out_t* out, const Scheme& sch) {
@@ -906,6 +969,87 @@ struct HostTrace {
     }
 };
 
+// Host loops compiled twice, AVX2 and baseline x86-64, picked at load time
+// (the attribute means nothing to the gfx950 pass of this file).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MSW_HOST_SIMD
+#else
+#define MSW_HOST_SIMD __attribute__((target_clones("avx2", "default")))
+#endif
+
+// One pass over a chunk's per-pair arrays: the read lengths, the window
+// lengths (genome mode: clipped at the genome end) and the positions into the
+// slot's metadata block, and what the dispatch needs -- the length bounds and
+// the cells and bytes.  Plain loops over the arrays (the compiler vectorises
+// them; AVX2 where the host has it): ~10k pairs per microsecond.
+struct ChunkScan {
+    uint32_t lm = 0xFFFF, gm = 0, ln = 0xFFFF, gn = 0;
+    uint64_t cells = 0, bytes = 0;
+};
+
+MSW_HOST_SIMD
+void scan_lengths(const uint16_t* __restrict rl, const uint16_t* __restrict wl, uint64_t n, ChunkScan& c) {
+    uint32_t lm = 0xFFFF, gm = 0, ln = 0xFFFF, gn = 0;
+    uint64_t cells = 0, bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t r = rl[i], w = wl[i];
+        lm = std::min(lm, r);
+        gm = std::max(gm, r);
+        ln = std::min(ln, w);
+        gn = std::max(gn, w);
+        cells += r * w;
+        bytes += r + w;
+    }
+    c.lm = lm, c.gm = gm, c.ln = ln, c.gn = gn, c.cells = cells, c.bytes = bytes;
+}
+
+MSW_HOST_SIMD
+void clip_windows(const int64_t* __restrict pos, const uint16_t* __restrict want, uint64_t n, uint64_t glen,
+                  uint16_t* __restrict out) {
+    for (uint64_t i = 0; i < n; ++i) out[i] = genome_window(pos[i], want[i], glen);
+}
+
+MSW_HOST_SIMD
+void max_u16(const uint16_t* __restrict a, uint64_t n, uint32_t& m) {
+    uint32_t v = 0;
+    for (uint64_t i = 0; i < n; ++i) v = std::max<uint32_t>(v, a[i]);
+    m = v;
+}
+
+ChunkScan stage_meta(Slot& s, const HostBatch& b, uint64_t first, uint64_t cnt) {
+    memcpy(s.h_rlen, b.read_len + first, cnt * sizeof(uint16_t));
+    if (b.genome) {
+        memcpy(s.h_pos, b.win_pos + first, cnt * sizeof(int64_t));
+        clip_windows(b.win_pos + first, b.win_len + first, cnt, b.genome->len, s.h_wlen);
+    } else {
+        memcpy(s.h_wlen, b.win_len + first, cnt * sizeof(uint16_t));
+    }
+    ChunkScan c;
+    scan_lengths(s.h_rlen, s.h_wlen, cnt, c);
+    return c;
+}
+
+// True when every pair of the chunk has one bucket key (bucket_chunk's: rows
+// per lane of its read, 16-column blocks of its window, not long) -- decided
+// from the bounds alone, both keys being monotone in the lengths.
+bool single_key(const ChunkScan& c) {
+    return !force_long() && !is_long(c.gm, c.gn) &&
+           msw::rows_per_lane(c.lm, false) == msw::rows_per_lane(c.gm, false) &&
+           (c.ln + 15) / 16 == (c.gn + 15) / 16;
+}
+
+// Pinned-ness of the caller's arrays, remembered for the last few ranges
+// (hipPointerGetAttributes twice per array and call is a visible share of a
+// small call).  A stale verdict only changes how a copy is made, never what
+// it copies: hipMemcpyAsync accepts pageable and pinned sources alike.
+bool pinned_cached(msw_ctx* ctx, const void* p, size_t bytes) {
+    for (const msw_ctx::PinnedRange& r : ctx->pinned_ranges)
+        if (r.p == p && r.bytes == bytes && p) return r.pinned;
+    const bool pinned = is_pinned(p, bytes);
+    ctx->pinned_ranges[ctx->pinned_next++ % 4] = {p, bytes, pinned};
+    return pinned;
+}
+
 int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out_t* out,
                    uint64_t chunk_pairs, bool sync) {
     Scheme sch;
@@ -927,8 +1071,8 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     // (genome mode bounds the requested window lengths: a clipped window is
     // never longer, and the positions need not be read here)
     uint32_t gm = 0, gn = 0;
-    for (uint64_t i = 0; i < n; ++i) gm = std::max<uint32_t>(gm, b.read_len[i]);
-    for (uint64_t i = 0; i < n; ++i) gn = std::max<uint32_t>(gn, b.win_len[i]);
+    max_u16(b.read_len, n, gm);
+    max_u16(b.win_len, n, gn);
     if (gm > b.read_stride || (!gmode && gn > b.win_stride))
         return fail(MSW_E_INVALID, "length exceeds stride (max read %u / stride %u, max window %u / stride %u)",
                     gm, b.read_stride, gn, b.win_stride);
@@ -936,8 +1080,8 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
 
     // Direct DMA from pinned caller arrays; otherwise stage through the slot's
     // pinned buffers with rows repacked to 16-byte-rounded strides.
-    const bool d_reads = is_pinned(b.reads, n * b.read_stride);
-    const bool d_wins = !gmode && is_pinned(b.wins, n * b.win_stride);
+    const bool d_reads = pinned_cached(ctx, b.reads, n * b.read_stride);
+    const bool d_wins = !gmode && pinned_cached(ctx, b.wins, n * b.win_stride);
     const uint32_t rs = d_reads ? b.read_stride : std::min(b.read_stride, std::max(16u, round16(gm)));
     const uint32_t ws = gmode ? std::max(16u, round16(gn))
                               : (d_wins ? b.win_stride : std::min(b.win_stride, std::max(16u, round16(gn))));
@@ -949,9 +1093,12 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     // the d2h stream.  A one-chunk call keeps all of its work on one compute
     // stream (no cross-stream events: ~5 HIP calls fewer per call, the host
     // cost that bounds a stream of small async batches); async calls
-    // alternate that stream, so consecutive calls still overlap.
+    // alternate that stream, so consecutive calls still overlap.  Its kernels
+    // store the results straight into the slot's mapped host block (no copy,
+    // no event after the kernels but the timing one).
     const bool multi_chunk = n > chunk;
     const bool alternate = multi_chunk || !sync;
+    const bool direct_out = !multi_chunk && !getenv("MSW_NO_DIRECT_OUT");
     std::vector<Bucket> buckets;
     uint64_t c = 0;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
@@ -983,35 +1130,29 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
             }
         }
         // Metadata block: lengths (effective window lengths in genome mode),
-        // positions, slot order.
-        memcpy(s.h_rlen, b.read_len + first, cnt * sizeof(uint16_t));
-        if (gmode) {
-            const int64_t* p = b.win_pos + first;
-            const uint16_t* req = b.win_len + first;
-            const uint64_t glen = b.genome->len;
-            for (uint64_t i = 0; i < cnt; ++i) {
-                s.h_pos[i] = p[i];
-                s.h_wlen[i] = genome_window(p[i], req[i], glen);
-            }
+        // positions; the slot order only for a chunk of several buckets.
+        const ChunkScan cs_ = stage_meta(s, b, first, cnt);
+        bool uniform;
+        if (single_key(cs_)) {  // fixed-length reads and windows, the common case: no sort
+            buckets.assign(1, Bucket{0, (uint32_t)cnt, cs_.gm, cs_.gn});
+            uniform = true;
         } else {
-            memcpy(s.h_wlen, b.win_len + first, cnt * sizeof(uint16_t));
+            uint32_t lens[4];
+            bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets, lens);
+            // One read-length bucket: order only matters if windows vary a lot;
+            // long pairs of spread read lengths keep their heaviest-first order.
+            uniform = buckets.size() == 1 && lens[3] - lens[2] < 16 &&
+                      (!buckets[0].long_pairs || lens[1] - lens[0] < 64);
         }
-        uint32_t lens[4];
-        bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets, lens);
-        // One read-length bucket: order only matters if windows vary a lot;
-        // long pairs of spread read lengths keep their heaviest-first order.
-        const bool uniform = buckets.size() == 1 && lens[3] - lens[2] < 16 &&
-                             (!buckets[0].long_pairs || lens[1] - lens[0] < 64);
         if (tr.on) tr.stage += tr.lap();
         // H2D on the copy stream, kernels on the compute stream (a one-chunk
         // call: everything on its compute stream).
         hipStream_t up = multi_chunk ? ctx->copy : cs;
         HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
         if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
-        // [pos | order | rlen | wlen]: skip the parts this chunk does not use
-        const size_t meta_lo = gmode ? 0 : (uniform ? 12 : 8) * cnt;
-        HIP_TRY(hipMemcpyAsync(s.d_meta + meta_lo, s.h_meta + meta_lo, kMetaBytesPerPair * cnt - meta_lo,
-                               hipMemcpyHostToDevice, up));
+        // [pos | rlen | wlen | order]: the contiguous part this chunk uses
+        const size_t meta_lo = gmode ? 0 : 8 * cnt, meta_hi = (uniform ? 12 : 16) * cnt;
+        HIP_TRY(hipMemcpyAsync(s.d_meta + meta_lo, s.h_meta + meta_lo, meta_hi - meta_lo, hipMemcpyHostToDevice, up));
         // Pipelined: H2D + window cut on the copy stream, the scoring launch on
         // the compute stream, results back on the d2h stream -- chunk k+1's
         // uploads and chunk k-1's readback overlap chunk k's kernel.
@@ -1026,32 +1167,32 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
             buckets.resize(1);
             buckets[0].begin = 0;
         }
+        s.k_score = direct_out ? s.h_score : s.d_score;
+        s.k_ei = direct_out ? s.h_ei : s.d_ei;
+        s.k_ej = direct_out ? s.h_ej : s.d_ej;
         HIP_TRY(hipEventRecord(s.k_start, cs));
         if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws, cs))) return rc;
         HIP_TRY(hipEventRecord(s.k_end, cs));
-        {
-            uint64_t cells = 0, bytes = 0;
-            for (uint64_t i = 0; i < cnt; ++i) {
-                cells += (uint64_t)s.h_rlen[i] * s.h_wlen[i];
-                bytes += (uint64_t)s.h_rlen[i] + s.h_wlen[i];
+        ctx->stats.launches += 1;
+        ctx->stats.pairs += cnt;
+        ctx->stats.cells += cs_.cells;
+        ctx->stats.alg_bytes += cs_.bytes + cnt * (sch.coords ? 8u : 4u);
+        if (!direct_out) {
+            hipStream_t down = cs;
+            if (multi_chunk) {
+                HIP_TRY(hipEventRecord(s.computed, cs));
+                HIP_TRY(hipStreamWaitEvent(ctx->d2h, s.computed, 0));
+                down = ctx->d2h;
             }
-            ctx->stats.launches += 1;
-            ctx->stats.pairs += cnt;
-            ctx->stats.cells += cells;
-            ctx->stats.alg_bytes += bytes + cnt * (sch.coords ? 8u : 4u);
+            HIP_TRY(hipMemcpyAsync(s.h_res, s.d_res, (sch.coords ? kResBytesPerPair : 4) * cnt,
+                                   hipMemcpyDeviceToHost, down));
+            HIP_TRY(hipEventRecord(s.done, down));
         }
-        hipStream_t down = cs;
-        if (multi_chunk) {
-            HIP_TRY(hipEventRecord(s.computed, cs));
-            HIP_TRY(hipStreamWaitEvent(ctx->d2h, s.computed, 0));
-            down = ctx->d2h;
-        }
-        HIP_TRY(hipMemcpyAsync(s.h_res, s.d_res, (sch.coords ? kResBytesPerPair : 4) * cnt, hipMemcpyDeviceToHost,
-                               down));
-        HIP_TRY(hipEventRecord(s.done, down));
         s.busy = true;
+        s.direct_out = direct_out;
         s.by_slot = !uniform;
         s.ticket = ctx->next_ticket;  // the ticket an async call returns
+        s.seq = seq;
         s.first = first;
         s.count = cnt;
         s.out = *out;
@@ -1059,18 +1200,17 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     }
     if (tr.on) tr.submit += tr.lap();  // the last chunk's HIP calls
     if (sync) {
-        for (Slot& sl : ctx->slots)
-            if ((rc = drain_slot(ctx, sl))) return rc;
+        if ((rc = drain_through(ctx, UINT64_MAX))) return rc;
         if (tr.on) tr.wait += tr.lap();
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));
     }
     if (tr.on)
         fprintf(stderr,
-                "[msw host] pairs=%llu chunks=%llu direct(reads=%d wins=%d) rs=%u ws=%u "
+                "[msw host] pairs=%llu chunks=%llu direct(reads=%d wins=%d out=%d) rs=%u ws=%u "
                 "scan=%.1fus stage=%.1fus submit=%.1fus wait=%.1fus\n",
-                (unsigned long long)n, (unsigned long long)c, (int)d_reads, (int)d_wins, rs, ws, tr.scan,
-                tr.stage, tr.submit, tr.wait);
+                (unsigned long long)n, (unsigned long long)c, (int)d_reads, (int)d_wins, (int)direct_out, rs, ws,
+                tr.scan, tr.stage, tr.submit, tr.wait);
     return MSW_OK;
 }
 
@@ -1230,6 +1370,7 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     for (hipEvent_t e : ctx->free_events) (void)hipEventDestroy(e);
     for (auto& kv : ctx->fences) (void)hipEventDestroy(kv.second);
     if (ctx->epoch) (void)hipEventDestroy(ctx->epoch);
+    if (ctx->epoch_next) (void)hipEventDestroy(ctx->epoch_next);
     if (ctx->compute) (void)hipStreamDestroy(ctx->compute);
     if (ctx->compute2) (void)hipStreamDestroy(ctx->compute2);
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
@@ -1261,8 +1402,7 @@ int msw_wait(msw_ctx* ctx, uint64_t ticket) {
     if (rc) return rc;
     // Drain the chunks of this ticket and of every earlier one (tickets are
     // enqueued in order on the same streams); later calls stay in flight.
-    for (Slot& s : ctx->slots)
-        if (s.busy && s.ticket <= ticket && (rc = drain_slot(ctx, s))) return rc;
+    if ((rc = drain_through(ctx, ticket))) return rc;
     ctx->done_ticket = std::max(ctx->done_ticket, ticket);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MSW_E_DEVICE, "kernel failure: %s", hipGetErrorString(e));

@@ -14,6 +14,33 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import LINE_LIMIT, compact_line  # noqa: E402
+
+
+def test_compact_line_fits_the_driver_tail():
+    """The one-line record of a full default run (round 4's, committed under
+    profiles/) stays under LINE_LIMIT and keeps every leg's rate, parity,
+    CPU baseline, VALU fraction and traffic ratio in its summary."""
+    with open(os.path.join(ROOT, "profiles", "r04", "final5", "bench_default.json")) as f:
+        full = json.load(f)
+    line = compact_line(full, "gpurun_out/bench_detail_n1.json")
+    assert len(json.dumps(line).encode()) <= LINE_LIMIT
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert line[k] == full[k] if k not in ("config", "roofline", "cpu_baseline") else line[k], k
+    assert line["roofline"]["frac"] == full["roofline"]["frac"] and line["roofline"]["traffic"] > 0
+    assert line["cpu_baseline"]["value"] == full["cpu_baseline"]["value"] and line["cpu_baseline"]["sample"]
+    s = line["summary"]
+    assert s["c2"]["bit_exact"] is True and s["c2"]["checked"] == 10000
+    assert s["c3_hbm"]["valu_frac"] == full["configs_extra"]["config3"]["valu"]["frac"]
+    assert s["c3_hbm"]["traffic_over_alg"] == 1.11 and s["c5_hbm"]["traffic_over_alg"] == 1.328
+    assert s["c3_fastq"]["checked"] == 1_000_000 and s["c3_fastq"]["bit_exact"] is True
+    assert s["c4"]["checked"] == 16 and s["c4"]["reads_per_s"] == full["configs_extra"]["config4"]["reads_per_s"]
+    assert s["c3_h2h"]["bit_exact"] is True and s["pcie"]["submit_us"] == 57.6
+    for leg in ("c2", "c3_hbm", "c5_hbm", "c4"):
+        assert s[leg]["cpu_gcups"] > 0, leg
 
 
 @pytest.mark.gpu
@@ -21,12 +48,26 @@ def test_bench_json_line(tmp_path):
     cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--pairs", "2000",
            "--cpu-seconds", "1", "--no-pcie", "--c3-pairs", "20000", "--c5-pairs", "10000",
            "--c4-reads-per-file", "20000", "--c4-segment-reads", "10000", "--c4-pool", "3",
-           "--c3-fastq-reads", "16000", "--c4-dir", str(tmp_path / "c4")]
+           "--c3-fastq-reads", "16000", "--c4-dir", str(tmp_path / "c4"),
+           "--detail", str(tmp_path / "detail.json")]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.strip().splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
+    line = json.loads(lines[0])
+    # the line fits the driver's output tail; every leg is in its summary
+    assert len(lines[0].encode()) <= LINE_LIMIT, len(lines[0])
+    summ = line["summary"]
+    for leg in ("c2", "c3_hbm", "c3_h2h", "c3_fastq", "c4", "c5_hbm"):
+        assert summ[leg]["bit_exact"] is True and summ[leg]["checked"] > 0, (leg, summ[leg])
+    for leg in ("c2", "c3_hbm", "c5_hbm"):
+        assert summ[leg]["cpu_gcups"] > 0 and 0 < summ[leg]["valu_frac"] < 1.5, (leg, summ[leg])
+    assert summ["c3_fastq"]["checked"] == 16000 and summ["c4"]["checked"] == 16
+    for k in ("roofline", "cpu_baseline", "parity", "valu"):
+        assert line[k], k
+    with open(tmp_path / "detail.json") as f:
+        d = json.load(f)
+    assert line["value"] == d["value"] and line["roofline"]["frac"] == d["roofline"]["frac"]
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         base = json.load(f)
     assert d["metric"] == base["metric"]

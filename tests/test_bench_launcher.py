@@ -34,9 +34,19 @@ def _env():
 
 
 def _json_line(out):
+    """The full record (the detail file the one-line record names), with the
+    line itself under "_line"; the line's own summary is checked here."""
     lines = [l for l in out.strip().splitlines() if l.startswith("{")]
     assert len(lines) == 1, out[-2000:]
-    return json.loads(lines[0])
+    line = json.loads(lines[0])
+    path = line["detail"]
+    with open(path if os.path.isabs(path) else os.path.join(ROOT, path)) as f:
+        full = json.load(f)
+    for k in ("metric", "value", "n_gpus", "steps", "warmup", "config", "roofline", "collectives"):
+        assert k in line, k
+    assert line["summary"]["c2"]["gcups"] == full["value"]
+    full["_line"] = line
+    return full
 
 
 def _check(d, world, per_gpu=3000):
@@ -57,24 +67,26 @@ def _port():
     return p
 
 
-def test_self_launch_two_ranks():
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + ARGS, cwd=ROOT, env=_env(),
+def test_self_launch_two_ranks(tmp_path):
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + ARGS + ["--detail", str(tmp_path / "d.json")],
+                       cwd=ROOT, env=_env(),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     _check(_json_line(r.stdout), 2)
 
 
-def test_torchrun_two_ranks():
+def test_torchrun_two_ranks(tmp_path):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2"]
-                       + ARGS, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+                       + ARGS + ["--detail", str(tmp_path / "d.json")],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     _check(_json_line(r.stdout), 2)
 
 
-def test_single_rank_standin():
-    r = subprocess.run([sys.executable, "bench.py"] + ARGS, cwd=ROOT, env=_env(), capture_output=True,
-                       text=True, timeout=300)
+def test_single_rank_standin(tmp_path):
+    r = subprocess.run([sys.executable, "bench.py"] + ARGS + ["--detail", str(tmp_path / "d.json")],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     _check(_json_line(r.stdout), 1)
 
@@ -104,13 +116,19 @@ def _check_extras(d, world):
     f3 = ex["config3"]["fastq"]  # per-read records of 2N lane files, gathered in file order
     assert f3["n_ranks"] == world and f3["reads"] == 320 * world and f3["scaling"] == "weak"
     assert f3["parity"]["bit_exact"] is True and f3["parity"]["records_checked"] == 320 * world
+    # one rank's two lane files generated and scored, byte-identical copies for the rest
+    ds = f3["dataset"]
+    assert ds["files_generated"] == 2 and ds["files_copied"] == 2 * world - 2, ds
+    assert ds["distinct_reads"] == 320 and ds["cells"] > 0
+    # config 4's lane set does not depend on N: 16 files of 3 pooled segments
+    assert c4["dataset"]["segments_total"] == 5 and c4["parity"]["reads_expected"] == 16 * 120
     col = d["collectives"]
     assert col["backend"] == "gloo" and col["world"] == world and col["calls_rank0"]["all_gather:int16->int32"] >= 1
 
 
 @pytest.mark.parametrize("launch", ["self", "torchrun"])
 def test_two_ranks_run_every_config(tmp_path, launch):
-    args = EXTRA + ["--c4-dir", str(tmp_path / "c4")]
+    args = EXTRA + ["--c4-dir", str(tmp_path / "c4"), "--detail", str(tmp_path / "d.json")]
     if launch == "self":
         cmd = [sys.executable, "bench.py", "--gpus", "2"] + args
     else:
@@ -127,7 +145,8 @@ def test_eight_ranks_run_every_config(tmp_path):
     """The driver's largest N: 8 ranks (gloo stand-in), every leg sharded and
     gathered -- config 4's 16 lane files two per rank, config 3's FASTQ lane
     per rank, configs 3 / 5 in order."""
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8"] + EXTRA + ["--c4-dir", str(tmp_path / "c4")],
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8"] + EXTRA + ["--c4-dir", str(tmp_path / "c4"),
+                                                                     "--detail", str(tmp_path / "d.json")],
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
@@ -136,7 +155,8 @@ def test_eight_ranks_run_every_config(tmp_path):
 
 
 def test_one_rank_runs_every_config(tmp_path):
-    r = subprocess.run([sys.executable, "bench.py"] + EXTRA + ["--c4-dir", str(tmp_path / "c4")], cwd=ROOT,
+    r = subprocess.run([sys.executable, "bench.py"] + EXTRA + ["--c4-dir", str(tmp_path / "c4"),
+                                                               "--detail", str(tmp_path / "d.json")], cwd=ROOT,
                        env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)

@@ -275,6 +275,33 @@ def test_ctx_stats_kernel_time_is_a_union(gpu_ctx):
     assert 0 < st["kernel_ms"] <= wall_ms, (st["kernel_ms"], wall_ms)
 
 
+def test_ctx_stats_kernel_time_lower_bound(gpu_ctx):
+    """the union must not lose intervals either.  Async calls in
+    pairs, each pair waited on its second ticket, drain their slots oldest
+    chunk first whatever slots they landed in (slots rotate in threes, so
+    pairs of calls put the newer chunk in the lower slot every third pair);
+    with large one-chunk launches the two calls of a pair barely overlap, so
+    their union is within a few percent of the same launches run one by one."""
+    b = config_batch(2, n_pairs=200_000, seed_offset=44)
+    sc = Scoring()
+
+    def run(k):
+        return gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc, chunk_pairs=200_000,
+                                   asynchronous=k is not None)
+    run(None)  # warm
+    gpu_ctx.stats(reset=True)
+    for _ in range(6):
+        run(None)
+    serial = gpu_ctx.stats(reset=True)["kernel_ms"]
+    for _ in range(3):
+        pend = [run(k) for k in range(2)]
+        pend[1].wait()
+        pend[0].wait()
+    paired = gpu_ctx.stats(reset=True)
+    assert paired["launches"] == 6
+    assert 0.9 * serial <= paired["kernel_ms"] <= 1.1 * serial, (paired["kernel_ms"], serial)
+
+
 def test_empty_batch(gpu_ctx):
     R = np.zeros((0, 16), np.uint8)
     s, i, j = gpu_ctx.align_batch(R, np.zeros(0, np.uint16), R, np.zeros(0, np.uint16), Scoring(want_coords=True))
