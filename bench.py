@@ -1102,7 +1102,8 @@ def _setup_split(rec):
     return [float(ph.get(k, 0.0)) for k in SETUP_PHASES]
 
 
-SETUP_PHASES = ("hip_init_ms", "reference_load_ms", "context_ms", "genome_ms", "result_sets_ms", "lane_reader_ms")
+SETUP_PHASES = ("hip_init_ms", "reference_load_ms", "context_ms", "genome_ms", "result_sets_ms", "lane_reader_ms",
+                "kernel_load_ms")
 # what each phase inside setup_ms is (named in the record when it binds)
 SETUP_WHY = {
     "context_ms": "the HIP runtime's device bring-up in the process's first stream creation (HSA queue "
@@ -1112,6 +1113,7 @@ SETUP_WHY = {
     "genome_ms": "each worker's copy of the reference into its context's HBM (pageable host memory)",
     "result_sets_ms": "the workers' pinned host result buffers and their device twins",
     "lane_reader_ms": "the GPU lane reader's span, inflate and parse buffers",
+    "kernel_load_ms": "the scoring kernels' code objects, loaded before the clock (msw_ctx_prepare)",
 }
 
 

@@ -251,6 +251,15 @@ typedef struct {
 } msw_stats_t;
 int msw_ctx_stats(msw_ctx* ctx, msw_stats_t* out, int reset);
 
+/* Optional, before a timed region: load the code objects of every scoring
+ * kernel module a call under this scheme may use (the packed layouts, the
+ * length-bucketed grid, genome windows, long pairs, the window cut).  HIP
+ * loads a module on its first launch, ~1-2 ms each, which a short run --
+ * one lane file per worker -- would otherwise pay inside its first batch
+ * (the reference has no analogue: it JIT-builds its OpenCL program on every
+ * gpu_align call, aligner.rs:504-508).  Launches nothing. */
+int msw_ctx_prepare(msw_ctx* ctx, const msw_scoring_t* scoring);
+
 /* Thread-local message of the last failing call on this thread. */
 const char* msw_last_error(void);
 

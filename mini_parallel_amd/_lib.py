@@ -29,7 +29,7 @@ EXPORTED = (
     "msw_plan_create", "msw_align_batch_planned", "msw_plan_destroy",
     "msw_genome_create", "msw_genome_destroy", "msw_genome_length", "msw_align_reads",
     "msw_align_reads_async", "msw_genome_cut_device", "msw_ctx_stats", "msw_align_reads_device",
-    "msw_memcpy_d2h_async", "msw_fence_record", "msw_fence_wait",
+    "msw_memcpy_d2h_async", "msw_fence_record", "msw_fence_wait", "msw_ctx_prepare",
 )
 # include/msw_fastq.h
 FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_next_packed",
@@ -133,6 +133,7 @@ def _declare(L):
         "msw_fence_wait": (I, [P, ctypes.c_uint64]),
         "msw_synchronize": (I, [P]),
         "msw_ctx_stats": (I, [P, ctypes.POINTER(StatsT), I]),
+        "msw_ctx_prepare": (I, [P, ctypes.POINTER(ScoringT)]),
         "msw_last_error": (ctypes.c_char_p, []),
         "msw_version": (ctypes.c_char_p, []),
         "msw_fastq_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),

@@ -324,6 +324,12 @@ class Context:
                     pass
         return _Launch()
 
+    def prepare(self, scoring: Scoring = LINEAR) -> None:
+        """msw_ctx_prepare: load every scoring kernel module this scheme may
+        use now (HIP loads a module at its first launch), so a short timed
+        run does not pay for it."""
+        check(lib().msw_ctx_prepare(self.handle, ctypes.byref(_scoring_c(scoring))))
+
     def synchronize(self) -> None:
         check(lib().msw_synchronize(self.handle))
 

@@ -608,6 +608,7 @@ struct WgsReport {
     // inside setup_ms (workers run them side by side); hip_init is filled in
     // by main (the first HIP call, before setup_ms)
     double reference_load_ms = 0, context_ms = 0, genome_ms = 0, result_sets_ms = 0, lane_reader_ms = 0;
+    double kernel_load_ms = 0;  // msw_ctx_prepare: the scoring kernels' code objects, before the clock
     unsigned long long gz_in = 0, gz_out = 0;  // compressed / inflated bytes (GPU lane reader)
 };
 
@@ -647,13 +648,14 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
     const uint64_t chunk = get_chunk_size_reads();
     const bool sw = a.score_mode == "sw";
     std::mutex setup_mu;
-    double ph_ctx = 0, ph_gen = 0, ph_res = 0, ph_reader = 0;  // max over workers
-    auto setup_phase = [&](double c, double g, double r, double rd) {
+    double ph_ctx = 0, ph_gen = 0, ph_res = 0, ph_reader = 0, ph_kl = 0;  // max over workers
+    auto setup_phase = [&](double c, double g, double r, double rd, double kl) {
         std::lock_guard<std::mutex> lk(setup_mu);
         ph_ctx = std::max(ph_ctx, c);
         ph_gen = std::max(ph_gen, g);
         ph_res = std::max(ph_res, r);
         ph_reader = std::max(ph_reader, rd);
+        ph_kl = std::max(ph_kl, kl);
     };
     auto report_setup = [&](WgsReport& rep) {
         rep.reference_load_ms = ref.ms;
@@ -661,6 +663,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         rep.genome_ms = ph_gen;
         rep.result_sets_ms = ph_res;
         rep.lane_reader_ms = ph_reader;
+        rep.kernel_load_ms = ph_kl;
     };
     if (sw && a.reference.empty()) die("error: --score-mode sw with --full-wgs needs --reference <FASTA>");
     // the reference: loading since the top of main, beside the HIP runtime
@@ -698,6 +701,14 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         long long cur = t_done_ns.load();
         while (t > cur && !t_done_ns.compare_exchange_weak(cur, t)) {
         }
+    };
+    // MSW_CLI_TRACE=1: per worker, ms since the start gate of each batch's
+    // arrival from the reader, its submission, and its settle (stderr)
+    static const bool cli_trace = getenv("MSW_CLI_TRACE") != nullptr;
+    auto trace_ev = [&](int wi, const char* what, uint64_t n) {
+        if (cli_trace)
+            fprintf(stderr, "[cli trace] worker %d %s n=%llu t=%.3f ms\n", wi, what, (unsigned long long)n,
+                    ms_since(t_all));
     };
     auto wall_and_teardown = [&](WgsReport& rep) {
         const double total = ms_since(t_all);
@@ -780,6 +791,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 const std::string& ref_seq = genome();
                 if (msw_genome_create(ctx.h, (const uint8_t*)ref_seq.data(), ref_seq.size(), &gen) != MSW_OK)
                     die(std::string("GPU genome upload error: ") + msw_last_error());
+                // the scoring kernels' modules, loaded now rather than at the first batch
+                const double t_kl0 = ms_since(ts0);
+                if (msw_ctx_prepare(ctx.h, &sc) != MSW_OK) die(std::string("GPU kernel load: ") + msw_last_error());
+                const double t_kl = ms_since(ts0) - t_kl0;
                 const double t_gen = ms_since(ts0);
                 // two result sets: batch k's copy-back lands while batch k+1 runs
                 struct Res {
@@ -816,6 +831,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     if (!r.live) return;
                     r.live = false;
                     FileState& f = *st[r.fi];
+                    trace_ev(wi, "settle-wait", r.n);
                     if (msw_fence_wait(ctx.h, r.fence) != MSW_OK) {
                         fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
                         f.failed = true;
@@ -839,14 +855,13 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         f.reads += r.n;
                         cells += cl;
                         if (f.scores_fd >= 0) {
-                            std::vector<uint8_t> out(r.n * 8);
-                            for (uint64_t i = 0; i < r.n; ++i) {
-                                memcpy(&out[i * 8], &sc32[i], 4);
-                                memcpy(&out[i * 8 + 4], &ei[i], 2);
-                                memcpy(&out[i * 8 + 6], &ej[i], 2);
-                            }
-                            if (pwrite(f.scores_fd, out.data(), out.size(), (off_t)(r.first * 8)) !=
-                                (ssize_t)out.size()) {
+                            // records [score i32 | end_i i16 | end_j i16], built as whole words
+                            // in a buffer that is not zeroed first
+                            std::unique_ptr<uint64_t[]> out(new uint64_t[r.n]);
+                            for (uint64_t i = 0; i < r.n; ++i)
+                                out[i] = (uint64_t)(uint32_t)sc32[i] | (uint64_t)(uint16_t)ei[i] << 32 |
+                                         (uint64_t)(uint16_t)ej[i] << 48;
+                            if (pwrite(f.scores_fd, out.get(), r.n * 8, (off_t)(r.first * 8)) != (ssize_t)(r.n * 8)) {
                                 fprintf(stderr, "  error writing scores for %s\n", f.path.c_str());
                                 f.failed = true;
                             }
@@ -854,9 +869,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     }
                     open_files[r.fi].first -= 1;
                     maybe_finish(r.fi);
+                    trace_ev(wi, "settled", r.n);
                 };
                 int cur = 0;
-                setup_phase(t_ctx, t_gen - t_rd, ms_since(ts0) - t_gen, t_rd - t_ctx);
+                setup_phase(t_ctx, t_gen - t_rd - t_kl, ms_since(ts0) - t_gen, t_rd - t_ctx, t_kl);
                 // the reader's stats of the file it just finished
                 auto reader_done = [&](size_t fi) {
                     uint64_t bi = 0, bo = 0;
@@ -922,6 +938,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         have = open_next(&fi);
                         continue;
                     }
+                    trace_ev(wi, "batch", d.n);
                     if (d.n == 0) {
                         reader_done(fi);
                         have = open_next(&fi);
@@ -946,6 +963,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         have = open_next(&fi);
                         continue;
                     }
+                    trace_ev(wi, "submitted", d.n);
                     r.n = d.n;
                     r.first = d.first_read;
                     r.fi = fi;
@@ -1096,7 +1114,9 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
             const uint64_t gsize = sw ? genome().size() : 0;
             if (sw && msw_genome_create(ctx.h, (const uint8_t*)genome().data(), gsize, &gen) != MSW_OK)
                 die(std::string("GPU genome upload error: ") + msw_last_error());
-            setup_phase(t_ctx, ms_since(ts0) - t_ctx, 0.0, 0.0);
+            const double t_gen = ms_since(ts0);
+            if (msw_ctx_prepare(ctx.h, &sc) != MSW_OK) die(std::string("GPU kernel load: ") + msw_last_error());
+            setup_phase(t_ctx, t_gen - t_ctx, 0.0, 0.0, ms_since(ts0) - t_gen);
             gate.arrive();
             // Up to three chunks in flight (msw_align_reads_async; msw_wait on the
             // oldest ticket before a fourth is staged): the context's three
@@ -1401,7 +1421,8 @@ int main(int argc, char** argv) {
           << ", \"gpu_inflate\": " << (rep.gpu_inflate ? "true" : "false") << ", \"setup_ms\": " << rep.setup_ms
           << ", \"setup_phases\": {\"hip_init_ms\": " << hip_init_ms << ", \"reference_load_ms\": " << rep.reference_load_ms
           << ", \"context_ms\": " << rep.context_ms << ", \"genome_ms\": " << rep.genome_ms
-          << ", \"result_sets_ms\": " << rep.result_sets_ms << ", \"lane_reader_ms\": " << rep.lane_reader_ms << "}"
+          << ", \"result_sets_ms\": " << rep.result_sets_ms << ", \"lane_reader_ms\": " << rep.lane_reader_ms
+          << ", \"kernel_load_ms\": " << rep.kernel_load_ms << "}"
           << ", \"teardown_ms\": " << rep.teardown_ms
           << ", \"inflate_bytes_in\": " << rep.gz_in << ", \"inflate_bytes_out\": " << rep.gz_out
           << ", \"reads_per_second\": " << reads / secs << "}\n";

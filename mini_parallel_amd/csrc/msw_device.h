@@ -122,6 +122,7 @@ struct PairMeta {
     uint32_t oa, ob;  // output indices: the pair's, or its slot's (p.out_by_slot)
     bool va, vb;
     int ma, mb, na, nb;
+    int64_t sa, sb;   // genome windows (GEN): first window byte in the genome (0 if empty)
 };
 
 // Traffic probes (tools/traffic_split.sh, built by tools/build_variant.sh with
@@ -141,7 +142,7 @@ struct PairMeta {
 #define MSW_PROBE_CONST_LEN 0
 #endif
 
-template <bool SPLIT>
+template <bool SPLIT, bool GEN>
 __device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t block, bool active) {
     // Branch-free: clamped indices keep every load legal (n_slots >= 1), the
     // lengths of padding slots (and of idle lanes) are masked to 0 afterwards.
@@ -180,7 +181,48 @@ __device__ __forceinline__ PairMeta load_meta(const SwParams& p, int g, uint32_t
     q.mb = q.vb ? mb : 0;
     q.na = q.va ? na : 0;
     q.nb = q.vb ? nb : 0;
+    if constexpr (GEN) {  // loaded beside the lengths (same round trip); an empty window reads the genome's start
+        const int64_t sa = p.win_pos[q.pa];
+        const int64_t sb = SPLIT ? sa : p.win_pos[q.pb];
+        q.sa = q.na > 0 ? sa : 0;
+        q.sb = q.nb > 0 ? sb : 0;
+    }
     return q;
+}
+
+// Window rows: a slab row (16-byte aligned, win_stride apart) or, for GEN
+// instances, a genome position (any alignment).
+template <bool GEN>
+__device__ __forceinline__ const uint8_t* win_row(const SwParams& p, uint32_t pair, int64_t pos) {
+    if constexpr (GEN) return p.win_src + pos;
+    else return p.wins + (uint64_t)pair * p.win_stride;
+}
+
+// 16 window bytes at row + 16 k: one 16-byte load from a slab row; from the
+// genome, the five dwords around the chunk (dword loads need only 4-byte
+// alignment) and one v_alignbyte per output dword.
+template <bool GEN>
+__device__ __forceinline__ uint4 win_chunk(const uint8_t* row, int k) {
+    const uint8_t* a = row + 16 * k;
+    if constexpr (!GEN) {
+        return *reinterpret_cast<const uint4*>(a);
+    } else {
+        // the dword base by pointer arithmetic (not an integer mask), so the
+        // compiler keeps the global address space: global, not flat, loads
+        const uint32_t b = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 3u);
+        const uint32_t* al = reinterpret_cast<const uint32_t*>(a - b);
+        const uint32_t x0 = al[0], x1 = al[1], x2 = al[2], x3 = al[3], x4 = al[4];
+        return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, b), __builtin_amdgcn_alignbyte(x2, x1, b),
+                          __builtin_amdgcn_alignbyte(x3, x2, b), __builtin_amdgcn_alignbyte(x4, x3, b));
+    }
+}
+
+// Last byte index a byte load of a window may use: the slab row's, or the
+// genome window's own (never past the genome).
+template <bool GEN>
+__device__ __forceinline__ int win_last(const SwParams& p, int n) {
+    if constexpr (GEN) return max(n, 1) - 1;
+    else return (int)p.win_stride - 1;
 }
 
 __device__ __forceinline__ int wave_max_i32(int v) {
@@ -212,30 +254,39 @@ __device__ __forceinline__ uint32_t wcode(uint32_t byte, bool valid, uint32_t sh
 // Sentinels past each window.  Vector path: 16-byte loads, a round of up to
 // two chunks of 16 columns per lane in flight together.  Scalar path
 // (unaligned batches): byte loads with clamped addresses, no branches.
-template <bool SPLIT>
+template <bool SPLIT, bool GEN>
 __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& q, uint32_t* stream,
                                              int steps, int lg, int G, bool active) {
     if (!active) return;
-    const uint8_t* wa = p.wins + (uint64_t)q.pa * p.win_stride;
-    const uint8_t* wb = p.wins + (uint64_t)q.pb * p.win_stride;
+    const uint8_t* wa = win_row<GEN>(p, q.pa, q.sa);
+    const uint8_t* wb = win_row<GEN>(p, q.pb, q.sb);
     const uint32_t sh = p.code_shift;
-    const int last = (int)p.win_stride - 1;
+    const int last = win_last<GEN>(p, q.na), last_b = win_last<GEN>(p, q.nb);
     for (int k = lg; k < kLead; k += G) stream[k] = kWinSentinel2;
     const int nch = (steps + 15) >> 4;  // chunks of 16 columns to stage
     if (p.win_vec) {
         const int loadable = (int)(p.win_stride >> 4);
+        // genome windows: chunk indices clamped to each window's last chunk
+        // (columns past the window are masked), every load unconditional
+        const int top_a = GEN ? max((q.na + 15) / 16 - 1, 0) : 0, top_b = GEN ? max((q.nb + 15) / 16 - 1, 0) : 0;
         for (int k0 = 0; k0 < nch; k0 += 2 * G) {
             uint4 va[2], vb[2];
             uint32_t prev[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int k = k0 + u * G + lg;
-                const bool ld = k < nch && k < loadable && !MSW_PROBE_NO_WIN;
-                va[u] = ld ? *reinterpret_cast<const uint4*>(wa + 16 * k) : make_uint4(0, 0, 0, 0);
-                if constexpr (SPLIT) {
-                    prev[u] = wa[min(max(16 * k - 1, 0), last)];
+                if constexpr (GEN) {
+                    va[u] = win_chunk<true>(wa, min(k, top_a));
+                    if constexpr (SPLIT) prev[u] = wa[min(max(16 * k - 1, 0), last)];
+                    else vb[u] = win_chunk<true>(wb, min(k, top_b));
                 } else {
-                    vb[u] = ld ? *reinterpret_cast<const uint4*>(wb + 16 * k) : make_uint4(0, 0, 0, 0);
+                    const bool ld = k < nch && k < loadable && !MSW_PROBE_NO_WIN;
+                    va[u] = ld ? *reinterpret_cast<const uint4*>(wa + 16 * k) : make_uint4(0, 0, 0, 0);
+                    if constexpr (SPLIT) {
+                        prev[u] = wa[min(max(16 * k - 1, 0), last)];
+                    } else {
+                        vb[u] = ld ? *reinterpret_cast<const uint4*>(wb + 16 * k) : make_uint4(0, 0, 0, 0);
+                    }
                 }
             }
 #pragma unroll
@@ -275,7 +326,7 @@ __device__ __forceinline__ void stage_window(const SwParams& p, const PairMeta& 
             for (int u = 0; u < 4; ++u) {
                 const int c = c0 + u * G + lg;
                 ba[u] = wa[min(c, last)];
-                bb[u] = SPLIT ? wa[min(max(c - 1, 0), last)] : wb[min(c, last)];
+                bb[u] = SPLIT ? wa[min(max(c - 1, 0), last)] : wb[min(c, GEN ? last_b : last)];
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -508,19 +559,20 @@ struct WinRound {
     uint32_t prev[kRound];  // split: the byte before each chunk
 };
 
-template <bool SPLIT>
+template <bool SPLIT, bool GEN>
 __device__ __forceinline__ void load_round(const SwParams& p, const PairMeta& q, int k0, int lg, int G,
                                            WinRound& w) {
-    const uint8_t* wa = p.wins + (uint64_t)q.pa * p.win_stride;
-    const uint8_t* wb = p.wins + (uint64_t)q.pb * p.win_stride;
+    const uint8_t* wa = win_row<GEN>(p, q.pa, q.sa);
+    const uint8_t* wb = win_row<GEN>(p, q.pb, q.sb);
     // last chunk to load per pair: the end of ITS window (not the launch's
     // longest, which a length bucket's short windows would over-read by up to
     // a 128-byte line each), and never past the row or the stream -- lanes
     // past it re-load that chunk (the same line, coalesced)
-    const int top = min((int)(p.win_stride >> 4), (int)((p.lds_stride - kLead) >> 4)) - 1;
+    const int stream_top = (int)((p.lds_stride - kLead) >> 4);
+    const int top = (GEN ? stream_top : min((int)(p.win_stride >> 4), stream_top)) - 1;
     const int top_a = max(min(top, ((q.na + 15) >> 4) - 1), 0);
     const int top_b = max(min(top, ((q.nb + 15) >> 4) - 1), 0);
-    const int last = (int)p.win_stride - 1;
+    const int last = win_last<GEN>(p, q.na);
 #pragma unroll
     for (int u = 0; u < kRound; ++u) {
         // clamped chunk index: always a legal load; columns past the window are masked
@@ -530,9 +582,9 @@ __device__ __forceinline__ void load_round(const SwParams& p, const PairMeta& q,
         w.prev[u] = 0;
         (void)wa; (void)wb; (void)last; (void)top_a; (void)top_b;
 #else
-        w.a[u] = *reinterpret_cast<const uint4*>(wa + 16 * min(k, top_a));
+        w.a[u] = win_chunk<GEN>(wa, min(k, top_a));
         if constexpr (SPLIT) w.prev[u] = wa[min(max(16 * k - 1, 0), last)];
-        else w.b[u] = *reinterpret_cast<const uint4*>(wb + 16 * min(k, top_b));
+        else w.b[u] = win_chunk<GEN>(wb, min(k, top_b));
 #endif
     }
 }
@@ -626,7 +678,7 @@ constexpr bool explicit_sched(bool affine, bool coords) { return !affine || coor
 constexpr int step_unroll(bool /*affine*/, bool coords) { return coords ? 2 : 4; }
 constexpr int perm_lead(bool affine, bool coords) { return !affine && !coords ? 2 : 0; }
 
-template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
+template <int KR, bool AFFINE, bool COORDS, bool SPLIT, bool GEN = false>
 __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint32_t* lds, uint64_t& t_loop) {
     const int lane = threadIdx.x;
     const int G = (int)p.group_lanes;
@@ -640,7 +692,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     // move folds into one v_and_b32_dpp instead of becoming a v_cndmask.
     uint32_t top_mask = lg == 0 ? 0u : ~0u;
     asm volatile("" : "+v"(top_mask));
-    const PairMeta q = load_meta<SPLIT>(p, g, block, active);
+    const PairMeta q = load_meta<SPLIT, GEN>(p, g, block, active);
     // Staging.  The lengths, the read bytes and the first round of window
     // chunks are all in flight before anything waits on the lengths (one
     // memory round trip); 16-byte aligned batches under an f16 scheme stage
@@ -650,7 +702,7 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
     load_read_bytes<KR, SPLIT>(p, q.pa, q.pb, lg, rb_a, rb_b);
     const bool try_fast = p.f16_ok && p.win_vec;
     WinRound w0;
-    if (try_fast) load_round<SPLIT>(p, q, 0, lg, G, w0);
+    if (try_fast) load_round<SPLIT, GEN>(p, q, 0, lg, G, w0);
     const int skew = SPLIT ? 2 * (G - 1) + 1 : G - 1;
     // wavefront steps, rounded up to a multiple of the steps per iteration
     // (the explicitly scheduled f16 loops of the pairs layout run four steps
@@ -669,14 +721,14 @@ __device__ __forceinline__ bool sw_body(const SwParams& p, uint32_t block, uint3
             bad = sel_round<SPLIT>(q, stream, 0, nch, lg, G, w0);
             for (int k0 = kRound * G; k0 < nch; k0 += kRound * G) {  // windows past 16 kRound G columns
                 WinRound w;
-                load_round<SPLIT>(p, q, k0, lg, G, w);
+                load_round<SPLIT, GEN>(p, q, k0, lg, G, w);
                 bad |= sel_round<SPLIT>(q, stream, k0, nch, lg, G, w);
             }
         }
         fast = __builtin_amdgcn_ballot_w64(bad != 0u) == 0;
-        if (!fast) stage_window<SPLIT>(p, q, stream, steps, lg, G, active);
+        if (!fast) stage_window<SPLIT, GEN>(p, q, stream, steps, lg, G, active);
     } else {
-        stage_window<SPLIT>(p, q, stream, steps, lg, G, active);
+        stage_window<SPLIT, GEN>(p, q, stream, steps, lg, G, active);
         __syncthreads();
         fast = to_fast_path(stream, kLead + steps, lg, G, active, p.code_shift, p.f16_ok != 0);
     }
@@ -1111,8 +1163,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
     return base + (r % 8u) * G + r / 8u;
 }
 
-// One layout for the whole grid.
-template <int KR, bool AFFINE, bool COORDS, bool SPLIT>
+// One layout for the whole grid (GEN: windows read from the resident genome).
+template <int KR, bool AFFINE, bool COORDS, bool SPLIT, bool GEN = false>
 __global__ __launch_bounds__(64) void sw_kernel(SwParams p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const WaveClock wc = trace_begin(p);
@@ -1120,7 +1172,7 @@ __global__ __launch_bounds__(64) void sw_kernel(SwParams p) {
     // identity block order: the XCD-grouped map below cut config 2's fetched
     // bytes 5.36 -> 4.99 MB per launch but slowed it 46.2 -> 50.2 us
     // (profiles/r03/traffic/xcd_remap_ab.jsonl); kept for the bucketed grid
-    const bool fast = sw_body<KR, AFFINE, COORDS, SPLIT>(p, blockIdx.x, lds, t_loop);
+    const bool fast = sw_body<KR, AFFINE, COORDS, SPLIT, GEN>(p, blockIdx.x, lds, t_loop);
     trace_end(p, wc, fast, SPLIT, KR, t_loop);
 }
 

@@ -678,6 +678,7 @@ int next_span(msw_gfastq* g) {
     }
     g->last_used = used;
     start_filler(g);
+    const double t_unpin = trace ? now_ms() : 0.0;
     const uint64_t nlines = g->h_out->lines;
     const bool any_high = g->h_out->any_high != 0;
     // 5. size the line arrays, phase B
@@ -701,9 +702,9 @@ int next_span(msw_gfastq* g) {
     if (trace)
         fprintf(stderr, "[gfastq] %s span: %zu members, %.1f MB in, %.1f MB out: read+index %.2f ms "
                         "(read-ahead join %.2f, window pin %.2f, index %.2f), "
-                        "inflate+parse A %.2f ms, parse B %.2f ms, %llu reads\n",
+                        "inflate+parse A %.2f ms, parse B %.2f ms (unpin + read-ahead start %.2f), %llu reads\n",
                 g->path.c_str(), g->mem.size(), used / 1e6, obytes / 1e6, t_read - t0, t_join - t0, t_reg - t_join,
-                t_read - t_reg, t_a - t_read, now_ms() - t_a, (unsigned long long)o.reads);
+                t_read - t_reg, t_a - t_read, now_ms() - t_a, t_unpin - t_a, (unsigned long long)o.reads);
     if (o.err_over)
         return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
                          (unsigned long long)o.err_line);
@@ -882,7 +883,12 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     // CU mask (here all CUs) is not placed on one of the GPU_MAX_HW_QUEUES
     // queues that plain streams share, where the --full-wgs traces showed one
     // worker's inflate and parse kernels queued with a scoring stream
-    // (DESIGN.md 6.2).  A plain stream if the masked one cannot be made.
+    // (DESIGN.md 6.2).  A CU-masked stream is a blocking stream (ordered with
+    // the null stream); the fallback, when the masked one cannot be made, is
+    // a blocking stream too, so the reader's ordering is the same either way:
+    // work a caller puts on the null stream (hipMemcpy, PyTorch's default
+    // stream) serialises with inflate and parse -- score on a stream of your
+    // own to overlap them (fastq.GpuFastqReader).
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || ncu <= 0)
@@ -894,7 +900,7 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
             g->rs = nullptr;
         }
     }
-    if ((!g->rs && hipStreamCreateWithFlags(&g->rs, hipStreamNonBlocking) != hipSuccess) ||
+    if ((!g->rs && hipStreamCreateWithFlags(&g->rs, hipStreamDefault) != hipSuccess) ||
         hipEventCreateWithFlags(&g->parsed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&g->emitted[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&g->emitted[1], hipEventDisableTiming) != hipSuccess)
@@ -918,6 +924,25 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
             (g->want_pos && hipMalloc((void**)&g->s_pos[i], (size_t)max_reads * 8 + kPad) != hipSuccess))
             return bail(set_error(MSW_E_NOMEM, "hipMalloc failed (GPU lane reader buffers, span %llu MiB)",
                                   (unsigned long long)(g->span >> 20)));
+    }
+    // Every device buffer a span needs, sized for a full span now (setup), so
+    // no hipMalloc runs between a file's first inflate and its first batch:
+    // in a short run (config 3 from FASTQ: one file per worker) those
+    // first-use allocations sat on the critical path, 2-4 ms each, and the
+    // workers' allocations serialised (profiles/r05/c3f/).  Line arrays
+    // assume lines of >= 32 bytes on average (FASTQ of 150 bp reads: ~90);
+    // a span with more lines still grows them.
+    {
+        const size_t lines = (size_t)(g->span / 32) + 1024;
+        const size_t members = (size_t)(g->span / 32768) + 1024;  // BGZF members hold <= 64 KiB
+        const size_t tiles = (size_t)((kCarry + g->span + 16 + msw::kParseTile - 1) / msw::kParseTile) + 1;
+        if ((rc = grow(&g->inf.dc, &g->inf.dc_cap, g->in_cap + 4096 + kInPad)) ||
+            (rc = grow(&g->inf.d_mem, &g->inf.mem_cap, members)) ||
+            (rc = grow(&g->inf.d_status, &g->inf.status_cap, members)) ||
+            (rc = grow(&g->tile_nl, &g->tile_cap, tiles)) || (rc = grow(&g->tile_hi, &g->tile_hi_cap, tiles)) ||
+            (rc = grow(&g->pb[0].line_end, &g->line_cap[0], lines)) ||
+            (rc = grow(&g->pb[1].line_end, &g->line_cap[1], lines)))
+            return bail(rc);
     }
     if (hipMalloc((void**)&g->d_state, sizeof(msw::ParseState)) != hipSuccess ||
         hipMalloc((void**)&g->d_state0, sizeof(msw::ParseState)) != hipSuccess ||

@@ -83,6 +83,13 @@ struct SwParams {
     // slots, a block that finishes a slot takes the next unclaimed one
     // (gridDim.x + counter) instead of striding by gridDim.x
     uint32_t* long_next;
+    // Genome-resident windows (instances with GEN = true: pairs layout, KR <=
+    // 16): the window of pair p is win_src[win_pos[p] ..], win_len[p] bytes
+    // (clipped by the host), read straight from the resident genome at any
+    // alignment instead of from a cut slab (wins / win_stride unused); the
+    // genome allocation extends >= 20 bytes past every window (kGenomePad).
+    const uint8_t* win_src;
+    const int64_t* win_pos;
 };
 
 // f16 bits of the cell value v * 2^-11 (|v| < 2048: exact, normal or zero).
@@ -135,6 +142,14 @@ struct MultiTable {
 
 hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, Layout layout,
                      hipStream_t stream);
+
+// Blocks (waves) per CU of the instance launch_sw / launch_sw_multi would run
+// for these arguments (its VGPRs and p's LDS), without launching; the query
+// loads the instance's code object (HIP loads a module on its first use).
+// 0 on error.  cut_blocks_per_cu: the same for the window cut kernel.
+int sw_blocks_per_cu(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, Layout layout);
+int sw_multi_blocks_per_cu(const SwParams& p, const MultiTable& t, bool affine, bool coords);
+int cut_blocks_per_cu();
 
 // All buckets of `t` in one launch; p.order is required (slot -> pair), the
 // per-bucket fields of p (n_slots, lds_stride, f16_ok) come from the table.

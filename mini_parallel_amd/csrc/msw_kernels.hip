@@ -108,9 +108,37 @@ __global__ __launch_bounds__(256) void gather_results_kernel(const uint32_t* __r
 // ---------------------------------------------------------------------------
 // Dispatch.
 // ---------------------------------------------------------------------------
+thread_local int* t_occupancy = nullptr;
+
+int sw_blocks_per_cu(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, Layout layout) {
+    int nb = 0;
+    t_occupancy = &nb;
+    const hipError_t e = launch_sw(p, affine, coords, max_read_len, layout, nullptr);
+    t_occupancy = nullptr;
+    return e == hipSuccess ? nb : 0;
+}
+
+int sw_multi_blocks_per_cu(const SwParams& p, const MultiTable& t, bool affine, bool coords) {
+    int nb = 0;
+    t_occupancy = &nb;
+    const hipError_t e = launch_sw_multi(p, t, affine, coords, nullptr);
+    t_occupancy = nullptr;
+    return e == hipSuccess ? nb : 0;
+}
+
+int cut_blocks_per_cu() {
+    int nb = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cut_windows_kernel, 256, 0) == hipSuccess ? nb : 0;
+}
+
 hipError_t launch_sw(const SwParams& p, bool affine, bool coords, uint32_t max_read_len, Layout layout,
                      hipStream_t stream) {
     if (p.n_slots == 0) return hipSuccess;
+    if (p.win_src) {  // genome windows: pairs layout, KR <= 16 only (the runtime checks with genome_layout_ok)
+        const int kr = rows_per_lane(max_read_len, false, p.group_lanes);
+        if (layout != Layout::kPairs || kr < 1 || kr > 16) return hipErrorInvalidValue;
+        return affine ? launch_genome_aff(p, coords, kr, stream) : launch_genome_lin(p, coords, kr, stream);
+    }
     if (layout == Layout::kMixed) {
         const uint32_t rest = p.n_slots - min(p.n_slots, p.pairs_blocks * pairs_per_wave(false, p.groups));
         const uint32_t blocks = p.pairs_blocks + (rest + p.groups - 1) / p.groups;

@@ -7,9 +7,27 @@
 
 namespace msw {
 
+// Occupancy query mode (kernel_blocks_per_cu, msw_runtime.cpp): while this
+// thread's t_occupancy is set, every launch_* below stores the blocks per CU
+// of the kernel instance it would launch (its VGPRs and LDS) instead of
+// launching.  The query also loads the instance's code object, so a caller
+// can take that first-use cost before a timed region (msw_ctx_prepare).
+extern thread_local int* t_occupancy;
+
+template <typename... Args>
+inline hipError_t launch_or_query(void (*kernel)(Args...), dim3 grid, size_t shm, hipStream_t stream, Args... args) {
+    if (t_occupancy) return hipOccupancyMaxActiveBlocksPerMultiprocessor(t_occupancy, kernel, 64, shm);
+    hipLaunchKernelGGL(kernel, grid, dim3(64), shm, stream, args...);
+    return hipGetLastError();
+}
+
 // pairs layout, KR = 1..16 (msw_launch_pairs_lin.hip / msw_launch_pairs_aff.hip)
 hipError_t launch_pairs_lin(const SwParams& p, bool coords, int kr, hipStream_t stream);
 hipError_t launch_pairs_aff(const SwParams& p, bool coords, int kr, hipStream_t stream);
+// pairs layout, KR = 1..16, windows from the resident genome (p.win_src;
+// msw_launch_genome_lin.hip / msw_launch_genome_aff.hip)
+hipError_t launch_genome_lin(const SwParams& p, bool coords, int kr, hipStream_t stream);
+hipError_t launch_genome_aff(const SwParams& p, bool coords, int kr, hipStream_t stream);
 // pairs layout, KR = 17..24 (G = 16: reads of 257..384 bases; msw_launch_pairs_wide.hip)
 hipError_t launch_pairs_wide(const SwParams& p, bool affine, bool coords, int kr, hipStream_t stream);
 // split layout, KR = 1..8 (msw_launch_split.hip)

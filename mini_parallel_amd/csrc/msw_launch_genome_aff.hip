@@ -1,4 +1,7 @@
-// msw_launch_pairs_aff.hip -- affine-gap SW kernels, pairs layout (KR = 1..16).
+// msw_launch_genome_aff.hip -- affine-gap SW kernels, pairs layout (KR = 1..16),
+// windows read straight from the HBM-resident genome (GEN instances,
+// SwParams::win_src): one-chunk msw_align_reads calls score without a window
+// cut launch.  Separate units so they build beside the slab instances.
 #include "msw_device.h"
 #include "msw_launch.h"
 
@@ -9,12 +12,12 @@ hipError_t go(const SwParams& p, bool coords, hipStream_t stream) {
     const uint32_t per_wave = pairs_per_wave(false, p.groups);
     const dim3 grid((p.n_slots + per_wave - 1) / per_wave);
     const size_t shm = lds_bytes(p.lds_stride, p.groups);
-    if (coords) return launch_or_query(sw_kernel<KR, true, true, false>, grid, shm, stream, p);
-    else return launch_or_query(sw_kernel<KR, true, false, false>, grid, shm, stream, p);
+    if (coords) return launch_or_query(sw_kernel<KR, true, true, false, true>, grid, shm, stream, p);
+    else return launch_or_query(sw_kernel<KR, true, false, false, true>, grid, shm, stream, p);
 }
 }  // namespace
 
-hipError_t launch_pairs_aff(const SwParams& p, bool coords, int kr, hipStream_t stream) {
+hipError_t launch_genome_aff(const SwParams& p, bool coords, int kr, hipStream_t stream) {
     switch (kr) {
         case 1: return go<1>(p, coords, stream);
         case 2: return go<2>(p, coords, stream);

@@ -8,13 +8,12 @@ template <int KRP>
 hipError_t go(const SwParams& p, bool affine, bool coords, uint32_t blocks, hipStream_t stream) {
     const size_t shm = lds_bytes(p.lds_stride, p.groups);
     if (affine) {
-        if (coords) hipLaunchKernelGGL((sw_mixed_kernel<KRP, true, true>), dim3(blocks), dim3(64), shm, stream, p);
-        else hipLaunchKernelGGL((sw_mixed_kernel<KRP, true, false>), dim3(blocks), dim3(64), shm, stream, p);
+        if (coords) return launch_or_query(sw_mixed_kernel<KRP, true, true>, dim3(blocks), shm, stream, p);
+        else return launch_or_query(sw_mixed_kernel<KRP, true, false>, dim3(blocks), shm, stream, p);
     } else {
-        if (coords) hipLaunchKernelGGL((sw_mixed_kernel<KRP, false, true>), dim3(blocks), dim3(64), shm, stream, p);
-        else hipLaunchKernelGGL((sw_mixed_kernel<KRP, false, false>), dim3(blocks), dim3(64), shm, stream, p);
+        if (coords) return launch_or_query(sw_mixed_kernel<KRP, false, true>, dim3(blocks), shm, stream, p);
+        else return launch_or_query(sw_mixed_kernel<KRP, false, false>, dim3(blocks), shm, stream, p);
     }
-    return hipGetLastError();
 }
 }  // namespace
 

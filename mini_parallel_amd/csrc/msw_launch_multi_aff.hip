@@ -6,9 +6,8 @@ namespace msw {
 
 hipError_t launch_multi_aff(const SwParams& p, const MultiTable& t, bool coords, uint32_t grid, size_t shm,
                             hipStream_t stream) {
-    if (coords) hipLaunchKernelGGL((sw_multi_kernel<true, true>), dim3(grid), dim3(64), shm, stream, p, t);
-    else hipLaunchKernelGGL((sw_multi_kernel<true, false>), dim3(grid), dim3(64), shm, stream, p, t);
-    return hipGetLastError();
+    if (coords) return launch_or_query(sw_multi_kernel<true, true>, dim3(grid), shm, stream, p, t);
+    else return launch_or_query(sw_multi_kernel<true, false>, dim3(grid), shm, stream, p, t);
 }
 
 }  // namespace msw

@@ -8,13 +8,12 @@ namespace msw {
 hipError_t launch_multi_wide(const SwParams& p, const MultiTable& t, bool affine, bool coords, uint32_t grid,
                              size_t shm, hipStream_t stream) {
     if (affine) {
-        if (coords) hipLaunchKernelGGL((sw_multi_kernel<true, true, true>), dim3(grid), dim3(64), shm, stream, p, t);
-        else hipLaunchKernelGGL((sw_multi_kernel<true, false, true>), dim3(grid), dim3(64), shm, stream, p, t);
+        if (coords) return launch_or_query(sw_multi_kernel<true, true, true>, dim3(grid), shm, stream, p, t);
+        else return launch_or_query(sw_multi_kernel<true, false, true>, dim3(grid), shm, stream, p, t);
     } else {
-        if (coords) hipLaunchKernelGGL((sw_multi_kernel<false, true, true>), dim3(grid), dim3(64), shm, stream, p, t);
-        else hipLaunchKernelGGL((sw_multi_kernel<false, false, true>), dim3(grid), dim3(64), shm, stream, p, t);
+        if (coords) return launch_or_query(sw_multi_kernel<false, true, true>, dim3(grid), shm, stream, p, t);
+        else return launch_or_query(sw_multi_kernel<false, false, true>, dim3(grid), shm, stream, p, t);
     }
-    return hipGetLastError();
 }
 
 }  // namespace msw

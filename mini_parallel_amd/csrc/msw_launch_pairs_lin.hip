@@ -7,11 +7,10 @@ namespace {
 template <int KR>
 hipError_t go(const SwParams& p, bool coords, hipStream_t stream) {
     const uint32_t per_wave = pairs_per_wave(false, p.groups);
-    const dim3 grid((p.n_slots + per_wave - 1) / per_wave), block(64);
+    const dim3 grid((p.n_slots + per_wave - 1) / per_wave);
     const size_t shm = lds_bytes(p.lds_stride, p.groups);
-    if (coords) hipLaunchKernelGGL((sw_kernel<KR, false, true, false>), grid, block, shm, stream, p);
-    else hipLaunchKernelGGL((sw_kernel<KR, false, false, false>), grid, block, shm, stream, p);
-    return hipGetLastError();
+    if (coords) return launch_or_query(sw_kernel<KR, false, true, false>, grid, shm, stream, p);
+    else return launch_or_query(sw_kernel<KR, false, false, false>, grid, shm, stream, p);
 }
 }  // namespace
 

@@ -7,16 +7,15 @@ namespace {
 template <int KR>
 hipError_t go(const SwParams& p, bool affine, bool coords, hipStream_t stream) {
     const uint32_t per_wave = pairs_per_wave(true, p.groups);
-    const dim3 grid((p.n_slots + per_wave - 1) / per_wave), block(64);
+    const dim3 grid((p.n_slots + per_wave - 1) / per_wave);
     const size_t shm = lds_bytes(p.lds_stride, p.groups);
     if (affine) {
-        if (coords) hipLaunchKernelGGL((sw_kernel<KR, true, true, true>), grid, block, shm, stream, p);
-        else hipLaunchKernelGGL((sw_kernel<KR, true, false, true>), grid, block, shm, stream, p);
+        if (coords) return launch_or_query(sw_kernel<KR, true, true, true>, grid, shm, stream, p);
+        else return launch_or_query(sw_kernel<KR, true, false, true>, grid, shm, stream, p);
     } else {
-        if (coords) hipLaunchKernelGGL((sw_kernel<KR, false, true, true>), grid, block, shm, stream, p);
-        else hipLaunchKernelGGL((sw_kernel<KR, false, false, true>), grid, block, shm, stream, p);
+        if (coords) return launch_or_query(sw_kernel<KR, false, true, true>, grid, shm, stream, p);
+        else return launch_or_query(sw_kernel<KR, false, false, true>, grid, shm, stream, p);
     }
-    return hipGetLastError();
 }
 }  // namespace
 

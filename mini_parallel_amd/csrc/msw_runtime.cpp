@@ -320,6 +320,8 @@ struct msw_ctx {
     };
     std::deque<DevTiming> dev_timings;
     std::vector<hipEvent_t> free_events;
+    msw::Layout last_layout = msw::Layout::kPairs;  // the last packed launch's plan (MSW_HOST_TRACE)
+    uint32_t last_group_lanes = 0, last_kr = 0;
     std::unordered_map<uint64_t, hipEvent_t> fences;  // msw_fence_record, not yet waited on
     uint64_t next_fence = 1;
 };
@@ -563,14 +565,16 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
             const uint32_t groups = 64 / G;
             if (G != 16 && msw::lds_bytes(stride, groups) > 65536) continue;
             const uint64_t per = msw::pairs_per_wave(split, groups);
-            // 17..24 rows in narrower groups (150 bp reads: G = 8, KR = 19, 152
+            // 17..19 rows in narrower groups (150 bp reads: G = 8, KR = 19, 152
             // rows, no idle lane) fit only 3-4 waves per SIMD (122 VGPRs, the
             // LDS of 8 window streams), which the model does not see: only for
             // batches of >= 48 waves per SIMD.  Measured against G = 16 at 1M
             // pairs 5-6 % faster (linear, linear + cell, affine + cell); at
             // 262k 4 % faster to 13 % slower, at 65k up to 18 % slower
             // (tools/group_lanes_probe.py)
-            if (!split && G != 16 && kr > 16 && !force_g && (n_pairs + per - 1) / per < 48 * simds) continue;
+            // (only the measured rows-per-lane range, 17..19: 150 bp reads)
+            if (!split && G != 16 && kr > 16 && !force_g && (kr > 19 || (n_pairs + per - 1) / per < 48 * simds))
+                continue;
             const double t = makespan((n_pairs + per - 1) / per, wave_instr(split, G), 0, 0.0);
             if (t < best_t * 0.995) {
                 best_t = t;
@@ -599,6 +603,15 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
         best = {msw::Layout::kSplit, 0, 16, 4};
     }
     return best;
+}
+
+// Whether one launch of n pairs under these bounds can read its windows from
+// the resident genome: the GEN instances exist for the pairs layout with up
+// to 16 rows per lane (the shapes of short-read chunks), not for long pairs.
+bool genome_windows_ok(uint64_t n, uint32_t max_m, uint32_t max_n, const Scheme& sch, int cu_count) {
+    if (is_long(max_m, max_n)) return false;
+    const LaunchPlan plan = choose_layout(n, max_m, max_n, sch, cu_count);
+    return plan.layout == msw::Layout::kPairs && msw::rows_per_lane(max_m, false, plan.group_lanes) <= 16;
 }
 
 // Buckets of one chunk: pairs grouped by rows-per-lane (read length / 16), and
@@ -752,13 +765,32 @@ int join_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
 // 8.5 vs 12.7 TCUPS linear).
 bool use_wide_multi(size_t n_wide) { return use_multi(n_wide); }
 
+// Where a launch's windows come from: the slot's cut slab (win_stride), or,
+// with a genome, straight from the resident genome at the slot's positions
+// (the packed kernels only; long pairs need the slab).
+void set_windows(msw::SwParams& p, const Slot& s, uint32_t win_stride, const msw_genome* g) {
+    if (g) {
+        p.wins = nullptr;
+        p.win_stride = 0;
+        p.win_src = g->d_seq;
+        p.win_pos = s.d_pos;
+        p.win_vec = 1;
+    } else {
+        p.wins = s.d_wins;
+        p.win_stride = win_stride;
+        p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+    }
+}
+
 int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const std::vector<Bucket>& buckets,
-                   bool use_order, uint32_t read_stride, uint32_t win_stride, hipStream_t cs) {
+                   bool use_order, uint32_t read_stride, uint32_t win_stride, hipStream_t cs,
+                   const msw_genome* g = nullptr) {
     const size_t n_short = short_buckets(buckets);
     SideFork side;
     if (n_short < buckets.size()) {  // long pairs: their own launch, beside any packed ones
         const Bucket& b = buckets.back();
         msw::SwParams p = base_params(sch);
+        if (g) return fail(MSW_E_INVALID, "internal: long pairs need the window slab");
         p.reads = s.d_reads;
         p.wins = s.d_wins;
         p.read_len = s.d_rlen;
@@ -779,6 +811,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         if (rc) return rc;
         if (n_short == 0) return MSW_OK;
     }
+    if (g && (use_order || buckets.size() != 1)) return fail(MSW_E_INVALID, "internal: genome windows need one bucket");
     const size_t n_multi = multi_buckets(buckets);
     size_t first_single = 0;
     if (use_order && use_multi(n_multi)) {
@@ -792,8 +825,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.end_i = sch.coords ? s.k_ei : nullptr;
         p.end_j = sch.coords ? s.k_ej : nullptr;
         p.read_stride = read_stride;
-        p.win_stride = win_stride;
-        p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+        set_windows(p, s, win_stride, g);
         p.group_lanes = 16;
         p.groups = 4;
         p.out_by_slot = 1;
@@ -817,8 +849,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.end_i = sch.coords ? s.k_ei : nullptr;
         p.end_j = sch.coords ? s.k_ej : nullptr;
         p.read_stride = read_stride;
-        p.win_stride = win_stride;
-        p.win_vec = msw::vec_ok(p.wins, p.win_stride);
+        set_windows(p, s, win_stride, g);
         p.group_lanes = 16;
         p.groups = 4;
         p.out_by_slot = 1;
@@ -842,15 +873,17 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
         p.end_i = sch.coords ? s.k_ei : nullptr;
         p.end_j = sch.coords ? s.k_ej : nullptr;
         p.read_stride = read_stride;
-        p.win_stride = win_stride;
+        set_windows(p, s, win_stride, g);
         p.n_slots = b.count;
         p.lds_stride = msw::stream_stride(b.max_n);
-        p.win_vec = msw::vec_ok(p.wins, p.win_stride);
         p.f16_ok = f16_fits(sch, b.max_m, b.max_n) ? 1u : 0u;
         const LaunchPlan plan = choose_layout(b.count, b.max_m, b.max_n, sch, ctx->cu_count);
         p.pairs_blocks = plan.pairs_blocks;
         p.group_lanes = plan.group_lanes;
         p.groups = plan.groups;
+        ctx->last_layout = plan.layout;
+        ctx->last_group_lanes = plan.group_lanes;
+        ctx->last_kr = (uint32_t)msw::rows_per_lane(b.max_m, plan.layout == msw::Layout::kSplit, plan.group_lanes);
         HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, b.max_m, plan.layout, cs));
     }
     if (side.ev) return join_side(ctx, cs, side);
@@ -1099,6 +1132,13 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     const bool multi_chunk = n > chunk;
     const bool alternate = multi_chunk || !sync;
     const bool direct_out = !multi_chunk && !getenv("MSW_NO_DIRECT_OUT");
+    // Genome mode: a chunk of one bucket that the model puts in the pairs
+    // layout with <= 16 rows per lane reads its windows straight from the
+    // resident genome (GEN kernel instances: no cut launch, one dependent
+    // step fewer per chunk); other chunks cut a window slab first
+    // (MSW_GENOME_CUT=1 forces the cut for every chunk; tests run both).
+    const bool genome_ok = gmode && !force_long() && !getenv("MSW_GENOME_CUT");
+    uint64_t fused_chunks = 0;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
@@ -1144,6 +1184,8 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
             uniform = buckets.size() == 1 && lens[3] - lens[2] < 16 &&
                       (!buckets[0].long_pairs || lens[1] - lens[0] < 64);
         }
+        const bool fused = genome_ok && uniform && genome_windows_ok(cnt, cs_.gm, cs_.gn, sch, ctx->cu_count);
+        fused_chunks += fused ? 1 : 0;
         if (tr.on) tr.stage += tr.lap();
         // H2D on the copy stream, kernels on the compute stream (a one-chunk
         // call: everything on its compute stream).
@@ -1156,7 +1198,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         // Pipelined: H2D + window cut on the copy stream, the scoring launch on
         // the compute stream, results back on the d2h stream -- chunk k+1's
         // uploads and chunk k-1's readback overlap chunk k's kernel.
-        if (gmode)
+        if (gmode && !fused)
             HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, b.genome->len, s.d_pos, s.d_wlen, s.d_wins, nullptr, ws,
                                             cnt, up));
         if (multi_chunk) {
@@ -1171,7 +1213,8 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         s.k_ei = direct_out ? s.h_ei : s.d_ei;
         s.k_ej = direct_out ? s.h_ej : s.d_ej;
         HIP_TRY(hipEventRecord(s.k_start, cs));
-        if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws, cs))) return rc;
+        if ((rc = launch_buckets(ctx, sch, s, cnt, buckets, !uniform, rs, ws, cs, fused ? b.genome : nullptr)))
+            return rc;
         HIP_TRY(hipEventRecord(s.k_end, cs));
         ctx->stats.launches += 1;
         ctx->stats.pairs += cnt;
@@ -1207,9 +1250,12 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     }
     if (tr.on)
         fprintf(stderr,
-                "[msw host] pairs=%llu chunks=%llu direct(reads=%d wins=%d out=%d) rs=%u ws=%u "
-                "scan=%.1fus stage=%.1fus submit=%.1fus wait=%.1fus\n",
-                (unsigned long long)n, (unsigned long long)c, (int)d_reads, (int)d_wins, (int)direct_out, rs, ws,
+                "[msw host] pairs=%llu chunks=%llu direct(reads=%d wins=%d out=%d) genome_chunks=%llu rs=%u ws=%u "
+                "last_launch(layout=%s G=%u KR=%u) scan=%.1fus stage=%.1fus submit=%.1fus wait=%.1fus\n",
+                (unsigned long long)n, (unsigned long long)c, (int)d_reads, (int)d_wins, (int)direct_out,
+                (unsigned long long)fused_chunks, rs, ws,
+                ctx->last_layout == msw::Layout::kSplit ? "split" : (ctx->last_layout == msw::Layout::kMixed ? "mixed" : "pairs"),
+                ctx->last_group_lanes, ctx->last_kr,
                 tr.scan, tr.stage, tr.submit, tr.wait);
     return MSW_OK;
 }
@@ -1436,6 +1482,22 @@ static int traced_launch(msw::SwParams p, const Scheme& sch, uint32_t max_read_l
     return MSW_OK;
 }
 
+// One packed-kernel launch of p (pointers, strides / window source and
+// n_slots set) under the given length bounds: layout from the makespan model.
+static int launch_packed(msw_ctx* ctx, const Scheme& sch, msw::SwParams& p, uint32_t max_read_len,
+                         uint32_t max_win_len, hipStream_t st) {
+    p.lds_stride = msw::stream_stride(max_win_len);
+    p.f16_ok = f16_fits(sch, max_read_len, max_win_len) ? 1u : 0u;
+    const LaunchPlan plan = choose_layout(p.n_slots, max_read_len, max_win_len, sch, ctx->cu_count);
+    p.pairs_blocks = plan.pairs_blocks;
+    p.group_lanes = plan.group_lanes;
+    p.groups = plan.groups;
+    const char* trace_path = getenv("MSW_WAVE_TRACE");
+    if (trace_path && *trace_path) return traced_launch(p, sch, max_read_len, plan, st, trace_path);
+    HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st));
+    return MSW_OK;
+}
+
 int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batch_t* b, msw_out_t* out,
                            uint32_t max_read_len, uint32_t max_win_len, void* stream) {
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
@@ -1464,17 +1526,8 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     // bounds past the packed kernels: the whole batch on the long-pair kernel
     if (force_long() || is_long(max_read_len, max_win_len))
         return launch_long(sch, p, b->n_pairs, max_read_len, max_win_len, false, ctx->cu_count, st);
-    p.lds_stride = msw::stream_stride(max_win_len);
     p.win_vec = msw::vec_ok(p.wins, p.win_stride);
-    p.f16_ok = f16_fits(sch, max_read_len, max_win_len) ? 1u : 0u;
-    const LaunchPlan plan = choose_layout(b->n_pairs, max_read_len, max_win_len, sch, ctx->cu_count);
-    p.pairs_blocks = plan.pairs_blocks;
-    p.group_lanes = plan.group_lanes;
-    p.groups = plan.groups;
-    const char* trace_path = getenv("MSW_WAVE_TRACE");
-    if (trace_path && *trace_path) return traced_launch(p, sch, max_read_len, plan, st, trace_path);
-    HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st));
-    return MSW_OK;
+    return launch_packed(ctx, sch, p, max_read_len, max_win_len, st);
 }
 
 }  // extern "C"
@@ -1792,6 +1845,8 @@ int msw_align_reads_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_geno
     int rc = set_device(ctx);
     if (rc) return rc;
     const uint32_t max_win = window ? window : std::min<uint32_t>(2u * max_read_len, (uint32_t)msw::kMaxWinLen);
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    harvest_dev_timings(ctx, false);
     const uint32_t ws = std::max<uint32_t>(16u, (max_win + 15u) & ~15u);
     const size_t wbytes = (size_t)n * ws;
     if (wbytes > ctx->r_wins_cap) {
@@ -1806,8 +1861,6 @@ int msw_align_reads_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_geno
         }
         wlen = ctx->r_wlen;
     }
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
-    harvest_dev_timings(ctx, false);
     HIP_TRY(msw::launch_cut_windows_for_reads(g->d_seq, g->len, win_pos, read_len, window, ctx->r_wins, wlen, ws, n,
                                               st));
     msw_batch_t b{reads, ctx->r_wins, read_len, wlen, read_stride, ws, n};
@@ -1871,6 +1924,48 @@ int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (rc) return rc;
     HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return MSW_OK;
+}
+
+int msw_ctx_prepare(msw_ctx* ctx, const msw_scoring_t* sc) {
+    if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
+    Scheme sch;
+    int rc;
+    if ((rc = make_scheme(sc, &sch))) return rc;
+    if ((rc = set_device(ctx))) return rc;
+    // one occupancy query per kernel module (translation unit): the query
+    // loads the module; the shapes are any valid ones of that unit
+    msw::SwParams p = base_params(sch);
+    p.n_slots = 1;
+    p.lds_stride = msw::stream_stride(300);
+    p.group_lanes = 16;
+    p.groups = 4;
+    p.pairs_blocks = 1;
+    int ok = 1;
+    ok &= msw::sw_blocks_per_cu(p, sch.affine, sch.coords, 16, msw::Layout::kPairs) > 0;    // pairs, KR <= 16
+    ok &= msw::sw_blocks_per_cu(p, sch.affine, sch.coords, 300, msw::Layout::kPairs) > 0;   // pairs, KR 17..24
+    ok &= msw::sw_blocks_per_cu(p, sch.affine, sch.coords, 32, msw::Layout::kSplit) > 0;    // split
+    ok &= msw::sw_blocks_per_cu(p, sch.affine, sch.coords, 32, msw::Layout::kMixed) > 0;    // mixed grid
+    msw::MultiTable t;
+    memset(&t, 0, sizeof(t));
+    t.n_buckets = 1;
+    t.block_end[0] = 1;
+    t.count[0] = 1;
+    t.lds_stride[0] = p.lds_stride;
+    static const uint32_t dummy_order = 0;
+    p.order = &dummy_order;  // never dereferenced: nothing launches
+    for (uint32_t kr : {1u, 17u}) {  // the bucketed grid and its wide instance
+        t.kr[0] = kr;
+        ok &= msw::sw_multi_blocks_per_cu(p, t, sch.affine, sch.coords) > 0;
+    }
+    p.order = nullptr;
+    static const uint8_t dummy_genome = 0;
+    p.win_src = &dummy_genome;  // genome-window instances
+    ok &= msw::sw_blocks_per_cu(p, sch.affine, sch.coords, 16, msw::Layout::kPairs) > 0;
+    p.win_src = nullptr;
+    ok &= msw::long_blocks_per_cu(sch.affine, sch.coords, 600, 600) > 0;
+    ok &= msw::cut_blocks_per_cu() > 0;
+    (void)hipGetLastError();
+    return ok ? MSW_OK : fail(MSW_E_DEVICE, "kernel module load failed");
 }
 
 int msw_ctx_stats(msw_ctx* ctx, msw_stats_t* out, int reset) {

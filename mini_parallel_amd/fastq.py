@@ -92,7 +92,14 @@ class GpuFastqReader:
     """The GPU-side lane reader (msw_gfastq_*, BGZF files): inflate, CRC,
     line split and record parse run on the context's GPU; next_batch()
     returns the batch's device arrays (valid until the call after next) and,
-    for tests, ``host=True`` copies them back."""
+    for tests, ``host=True`` copies them back.
+
+    Streams: inflate and parse run on the reader's own stream, a blocking
+    stream (ordered with the null stream, as a CU-masked HIP stream is).
+    Work the caller puts on the null stream -- PyTorch's default stream,
+    synchronous hipMemcpy -- therefore serialises with the reader; score on a
+    stream of your own (torch.cuda.Stream) to overlap scoring with the next
+    span's inflate."""
 
     def __init__(self, ctx, path: str, stride: int = 256, max_reads: int = 1 << 20, with_pos: bool = False,
                  span_bytes: int = 0):

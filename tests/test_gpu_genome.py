@@ -43,6 +43,18 @@ def host_windows(genome: np.ndarray, pos: np.ndarray, want: np.ndarray):
     return W, eff.astype(np.uint16)
 
 
+@pytest.fixture(autouse=True, params=["genome_windows", "cut_slab"])
+def window_source(request, monkeypatch):
+    """Every test of this module twice: the packed kernels reading each
+    window straight from the resident genome (the default), and the windows
+    first cut into a slab (MSW_GENOME_CUT=1, also the path of long pairs)."""
+    if request.param == "cut_slab":
+        monkeypatch.setenv("MSW_GENOME_CUT", "1")
+    else:
+        monkeypatch.delenv("MSW_GENOME_CUT", raising=False)
+    return request.param
+
+
 def assert_same(got, want, coords):
     s, i, j = got
     ws, wi, wj = want
@@ -116,6 +128,105 @@ def test_genome_tiny_and_unaligned(gpu_ctx, oracle):
         W, wl = host_windows(g, pos, want)
         assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), True)
         genome.close()
+
+
+def test_genome_with_other_bytes(gpu_ctx, oracle):
+    """A genome holding N and lower-case runs: waves whose windows hold any
+    byte outside A/C/G/T stage integer codes (the byte-load path for genome
+    windows), the rest take the f16 path; every window start alignment."""
+    rng = np.random.default_rng(13)
+    g = rng.choice(ACGT, 200_003)
+    for a in range(0, g.size, 5000):
+        g[a:a + 40] = ord("N")
+    g[1000:1100] = np.frombuffer(b"acgt" * 25, np.uint8)
+    n = 3000
+    pos = np.concatenate([np.arange(980, 980 + 64), rng.integers(0, g.size, n - 64)]).astype(np.int64)
+    rl = np.full(n, 150, np.uint16)  # one bucket: the chunk reads its windows from the genome
+    want = np.full(n, 300, np.uint16)
+    R = np.zeros((n, 160), np.uint8)
+    for k in range(n):
+        src = int(min(pos[k] + 75, g.size - int(rl[k])))
+        R[k, :rl[k]] = g[src:src + int(rl[k])]
+    genome = gpu_ctx.load_genome(g)
+    W, wl = host_windows(g, pos, want)
+    for sc in SCHEMES:
+        got = gpu_ctx.align_reads(genome, R, rl, pos, want, sc)
+        assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), sc.want_coords)
+    genome.close()
+
+
+@pytest.mark.parametrize("sc", SCHEMES, ids=["linear", "linear_coords", "affine_coords"])
+@pytest.mark.parametrize("n,chunk", [(10_000, 0), (9_000, 2_500), (37, 0)])
+def test_genome_uniform_chunks(gpu_ctx, oracle, sc, n, chunk, monkeypatch, capfd, window_source):
+    """Chunks of one length bucket (150 bp reads, 289..300-byte windows: the
+    config-2 shape from the genome) -- the chunks the scoring kernels score
+    with windows read straight from the genome: every window start residue
+    mod 16, windows clipped a few bytes short at the genome end, reads with
+    N; async calls as bench.py streams them.  MSW_HOST_TRACE shows the path."""
+    rng = np.random.default_rng(n + chunk)
+    g = rng.choice(ACGT, 3_000_017)
+    pos = rng.integers(0, g.size - 300, n).astype(np.int64)
+    pos[:16] = 1000 + np.arange(16)
+    pos[16:20] = g.size - np.array([300, 297, 292, 289])
+    rl = np.full(n, 150, np.uint16)
+    want = np.full(n, 300, np.uint16)
+    R = np.zeros((n, 160), np.uint8)
+    for k in range(n):
+        R[k, :150] = g[pos[k] + 70:pos[k] + 220] if pos[k] + 220 <= g.size else rng.choice(ACGT, 150)
+    R[5, 40:44] = ord("N")
+    genome = gpu_ctx.load_genome(g)
+    W, wl = host_windows(g, pos, want)
+    expect = oracle_run(oracle, R, rl, W, wl, sc)
+    monkeypatch.setenv("MSW_HOST_TRACE", "1")
+    capfd.readouterr()
+    assert_same(gpu_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk), expect, sc.want_coords)
+    trace = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")]
+    chunks = int(trace[-1].split("chunks=")[1].split()[0])
+    genome_chunks = int(trace[-1].split("genome_chunks=")[1].split()[0])
+    if window_source == "cut_slab":
+        assert genome_chunks == 0, trace[-1]
+    elif n == 10_000:  # the config-2 shape: one chunk, pairs layout (smaller chunks may take the split layout)
+        assert genome_chunks == chunks == 1, trace[-1]
+    pend = [gpu_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk, asynchronous=True)
+            for _ in range(3)]
+    for p in pend[::-1]:
+        assert_same(p.wait(), expect, sc.want_coords)
+    genome.close()
+
+
+@pytest.mark.parametrize("window", [0, 300, 97])
+def test_align_reads_device(gpu_ctx, oracle, window):
+    """msw_align_reads_device (the --full-wgs GPU reader's call): reads and
+    positions in HBM, windows of `window` bytes (0: twice the read length)
+    clipped at the genome end, their lengths written back; scores and best
+    cells against the host restatement."""
+    import ctypes
+
+    import torch
+    from mini_parallel_amd._lib import OutT, check, lib
+    g, R, rl, pos, _ = genome_case(7000, 900_007, seed=83)
+    want = (np.minimum(2 * rl.astype(np.int64), 4096) if window == 0 else np.full(rl.size, window)).astype(np.uint16)
+    genome = gpu_ctx.load_genome(g)
+    dev = torch.device("cuda", 0)
+    d_reads = torch.from_numpy(R).to(dev)
+    d_rl = torch.from_numpy(rl.view(np.int16)).to(dev)
+    d_pos = torch.from_numpy(pos).to(dev)
+    n = pos.size
+    score = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    ei = torch.zeros(n, dtype=torch.int16, device=dev)
+    ej = torch.zeros(n, dtype=torch.int16, device=dev)
+    wlen = torch.full((n,), -1, dtype=torch.int16, device=dev)
+    W, wl = host_windows(g, pos, want)
+    for sc in SCHEMES:
+        out = OutT(score.data_ptr(), ei.data_ptr(), ej.data_ptr())
+        check(lib().msw_align_reads_device(gpu_ctx.handle, ctypes.byref(sc.to_c()), genome.handle,
+                                           d_reads.data_ptr(), d_rl.data_ptr(), R.shape[1], d_pos.data_ptr(), n,
+                                           window, int(rl.max()), ctypes.byref(out), wlen.data_ptr(), None))
+        gpu_ctx.synchronize()
+        assert np.array_equal(wlen.cpu().numpy().view(np.uint16), wl)
+        got = (score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy())
+        assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), sc.want_coords)
+    genome.close()
 
 
 def test_genome_mixed_lengths_bucketed(gpu_ctx, oracle):

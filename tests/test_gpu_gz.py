@@ -437,3 +437,39 @@ def test_reader_batch_length_bound(gpu_ctx, tmp_path, max_reads, group):
             got += len(ln)
     assert got == n
     assert 2 <= wide <= 2 * group
+
+
+def test_reader_on_the_default_stream(gpu_ctx, tmp_path):
+    """the reader's stream is a blocking stream (ordered with the
+    null stream).  With PyTorch work queued on its default stream between
+    batches -- which then serialises with inflate and parse -- every batch
+    still reads exactly as the host reader reads it."""
+    import ctypes
+
+    import torch
+    from mini_parallel_amd._lib import DevReadsT, check, lib
+    p = tmp_path / "lane.fastq.gz"
+    p.write_bytes(bgzf_compress(fastq_text(9_000, 33), 6, block=4000))
+    hs, hl, _, _ = host_reads(str(p), 256)
+    dev = torch.device("cuda", 0)
+    x = torch.ones(1 << 22, device=dev)
+    L = lib()
+    got_s, got_l = [], []
+    with GpuFastqReader(gpu_ctx, str(p), 256, 1000, span_bytes=1 << 20) as g:
+        while True:
+            with torch.cuda.stream(torch.cuda.default_stream(dev)):
+                x = x * 1.0001 + 1.0  # default-stream work in flight while the reader inflates and parses
+            d = DevReadsT()
+            check(L.msw_gfastq_next(g._h, None, ctypes.byref(d)))
+            n = int(d.n)
+            if n == 0:
+                break
+            check(L.msw_synchronize(gpu_ctx.handle))  # the emit ran on the context's compute stream
+            s = np.zeros((n, 256), np.uint8)
+            ln = np.zeros(n, np.uint16)
+            check(L.msw_memcpy_d2h(gpu_ctx.handle, s.ctypes.data, d.reads, s.nbytes))
+            check(L.msw_memcpy_d2h(gpu_ctx.handle, ln.ctypes.data, d.read_len, ln.nbytes))
+            got_s.append(s)
+            got_l.append(ln)
+    assert np.array_equal(np.concatenate(got_l), hl) and np.array_equal(np.concatenate(got_s), hs)
+    assert torch.isfinite(x).all()

@@ -111,14 +111,24 @@ def test_config3_affine_coords_sample(gpu_ctx, layout, oracle):
 
 @pytest.mark.parametrize("sc", [Scoring(), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)],
                          ids=["linear", "affine_coords"])
-def test_narrow_groups_large_batch(gpu_ctx, oracle, monkeypatch, sc):
-    """A batch large enough (>= 48 waves per SIMD) that the layout model
-    takes narrow lane groups of 17..24 rows (150 bp reads: G = 8 or 9) on its
-    own, as one launch: every pair against the SIMD oracle."""
+def test_narrow_groups_large_batch(gpu_ctx, oracle, monkeypatch, capfd, sc):
+    """A batch large enough (>= 48 waves per SIMD of 16-pair waves, sized
+    from this GPU's CU count) that the layout model takes narrow lane groups
+    of 17..19 rows (150 bp reads: G = 8 or 9) on its own, as one launch --
+    the choice read back from MSW_HOST_TRACE -- and every pair against the
+    SIMD oracle."""
     for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
         monkeypatch.delenv(k, raising=False)
-    b = config_batch(3, n_pairs=800_000)
-    got = gpu_run(gpu_ctx, b, sc, chunk=800_000)
+    n = int(48 * 4 * mpa.get_gpu_devices()[0].cu_count * 16 * 1.02)
+    b = config_batch(3, n_pairs=n)
+    monkeypatch.setenv("MSW_HOST_TRACE", "1")
+    capfd.readouterr()
+    got = gpu_run(gpu_ctx, b, sc, chunk=n)
+    line = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")][-1]
+    plan = line.split("last_launch(")[1].split(")")[0]
+    g = int(plan.split("G=")[1].split()[0])
+    kr = int(plan.split("KR=")[1].split()[0])
+    assert "layout=pairs" in plan and g in (8, 9) and 17 <= kr <= 19, line
     s, i, j, _ = oracle.sw_batch_simd(b.reads, b.read_len, b.wins, b.win_len, match=sc.match, mismatch=sc.mismatch,
                                       gap_open=sc.gap_open, gap_extend=sc.gap_extend, affine=sc.affine,
                                       threads=THREADS, coords=sc.want_coords)
@@ -473,3 +483,13 @@ def test_config1_plumbing(gpu_ctx, oracle):
     assert f"Best cell: read {int(want[1][0])}, window {int(want[2][0])}" in out
     out = subprocess.run([cli, "-1", s1, "-2", s2, "--gpu"], capture_output=True, text=True, check=True).stdout
     assert f"GPU Alignment score: {oracle.compat_align(s1.encode(), s2.encode(), 1024, 1_000_000)}" in out
+
+
+def test_ctx_prepare_then_score(gpu_ctx, oracle):
+    """msw_ctx_prepare loads the scoring modules (no launch) for every scheme;
+    scoring right after is unchanged."""
+    b = config_batch(2, n_pairs=2000, seed_offset=45)
+    for sc in (Scoring(), Scoring(want_coords=True), Scoring(gap_open=3, gap_extend=1, affine=True),
+               Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)):
+        gpu_ctx.prepare(sc)
+        assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), sc.want_coords)

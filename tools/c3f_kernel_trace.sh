@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 D=$(python3 -c "import sys; sys.path.insert(0, '.'); import bench; a = bench.parse([]); bench.ensure_c3f_dataset(a, 1); print(bench.c3f_layout(a, 1)[0])")
 export WGS_DATA_DIR=$D WGS_SAMPLE_ID=SYN WGS_LANES=1 WGS_READS_PER_LANE=2 GPU_CHUNK_SIZE_READS=65536
-export MSW_GFASTQ_TRACE=1 MSW_GZ_TIMING=1
+export MSW_GFASTQ_TRACE=1 MSW_CLI_TRACE=1
 for k in 1 2; do
   W=$(mktemp -d /tmp/c3ftr_XXXX)
   WGS_RUN_ID=c3ftrace_$$_$k timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/trace$k" -o t --output-format csv -- \
