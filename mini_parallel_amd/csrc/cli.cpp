@@ -753,10 +753,24 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
         std::atomic<unsigned long long> gz_in{0}, gz_out{0};
         // reads per scoring launch; wide slabs (MSW_MAX_READ_LEN) keep a batch's
         // slab near 256 MiB (two per worker)
+        // per-read records (--scores-out) are host work per read: batches of
+        // 256k reads, so one batch's records are written while the next one
+        // scores (config 3 from FASTQ: 17.4-18.0 -> 16.3-16.4 ms per 1 M reads,
+        // profiles/r05/c3f/c3f_batch_ab.jsonl); sums only: 1 M-read batches
+        const uint64_t batch_default = a.scores_out.empty() ? (1u << 20) : (1u << 18);
         const uint64_t batch = std::max<uint64_t>(
-            chunk, std::min<uint64_t>(strtoull(env_or("MSW_GFASTQ_BATCH", std::to_string(1u << 20)).c_str(), nullptr, 10),
+            chunk, std::min<uint64_t>(strtoull(env_or("MSW_GFASTQ_BATCH", std::to_string(batch_default)).c_str(),
+                                               nullptr, 10),
                                       (256ull << 20) / read_stride()));
         std::atomic<size_t> next_file{0};
+        // A claimed file is pending (prefetched by its claimer) until a worker
+        // starts it; a worker left with nothing to claim takes another
+        // worker's pending file instead of idling (with few or
+        // uneven files the claim-ahead could leave one worker a whole file
+        // of work at the end).  0 = pending, 1 = started; indexed like st.
+        std::unique_ptr<std::atomic<int>[]> started(new std::atomic<int>[st.size()]);
+        for (size_t i = 0; i < st.size(); ++i) started[i] = 0;
+        auto start_file = [&](size_t fi) { int e = 0; return started[fi].compare_exchange_strong(e, 1); };
         std::vector<std::thread> workers;
         // two workers (contexts) per GPU by default: one file's inflate and
         // host reads overlap the other's scoring
@@ -890,9 +904,18 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 // (msw_gfastq_prefetch), so the next switch does not wait on it.
                 auto open_next = [&](size_t* fi_out) -> bool {
                     for (;;) {
-                        const size_t fi = pending != kNone ? pending : claim();
+                        size_t fi = pending != kNone ? pending : claim();
                         pending = kNone;
-                        if (fi == kNone) return false;
+                        if (fi == kNone) {  // nothing left to claim: another worker's pending file
+                            for (size_t k : todo)
+                                if (started[k].load() == 0 && start_file(k)) {
+                                    fi = k;
+                                    break;
+                                }
+                            if (fi == kNone) return false;
+                        } else if (!start_file(fi)) {
+                            continue;  // taken by an idle worker meanwhile
+                        }
                         FileState& f = *st[fi];
                         f.t0 = Clock::now();
                         open_files[fi] = {0, false};

@@ -565,15 +565,22 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
             const uint32_t groups = 64 / G;
             if (G != 16 && msw::lds_bytes(stride, groups) > 65536) continue;
             const uint64_t per = msw::pairs_per_wave(split, groups);
-            // 17..19 rows in narrower groups (150 bp reads: G = 8, KR = 19, 152
-            // rows, no idle lane) fit only 3-4 waves per SIMD (122 VGPRs, the
-            // LDS of 8 window streams), which the model does not see: only for
-            // batches of >= 48 waves per SIMD.  Measured against G = 16 at 1M
-            // pairs 5-6 % faster (linear, linear + cell, affine + cell); at
-            // 262k 4 % faster to 13 % slower, at 65k up to 18 % slower
-            // (tools/group_lanes_probe.py)
-            // (only the measured rows-per-lane range, 17..19: 150 bp reads)
-            if (!split && G != 16 && kr > 16 && !force_g && (kr > 19 || (n_pairs + per - 1) / per < 48 * simds))
+            // 17..19 rows in narrower groups (150 bp reads: G = 8 / KR = 19 or
+            // G = 9 / KR = 17) fit only 2-3 waves per SIMD (VGPRs; the LDS of 7-8
+            // window streams), and the makespan model does not predict where
+            // they start to win (an occupancy-rounds model puts
+            // them ahead at every size).  So the gate is the measured crossover
+            // per instance family (tools/group_lanes_probe.py, alternating A/B
+            // against G = 16, profiles/r05/ab/group_9v16.jsonl and
+            // profiles/r04/ab/group_lanes_probe_sizes.jsonl):
+            //  KR 17 (G = 9): 2-3 % slower at 9 waves per SIMD (131k pairs),
+            //    2.4-3.5 % faster at 18, 3.5-5 % at 37, 5-6 % at 55: >= 16;
+            //  KR 18..19 (G = 8): 4 % faster to 13 % slower at 16 waves per
+            //    SIMD (262k), 5-6 % faster at 64 (1M): >= 48.
+            // Larger rows-per-lane counts were never measured: not taken.
+            const uint64_t min_waves = kr <= 17 ? 16 : 48;
+            if (!split && G != 16 && kr > 16 && !force_g &&
+                (kr > 19 || (n_pairs + per - 1) / per < min_waves * simds))
                 continue;
             const double t = makespan((n_pairs + per - 1) / per, wave_instr(split, G), 0, 0.0);
             if (t < best_t * 0.995) {

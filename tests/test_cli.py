@@ -248,6 +248,31 @@ def test_full_wgs_config4_shape_two_workers(tmp_path, oracle, gpu_inflate):
 
 
 @pytest.mark.gpu
+def test_full_wgs_three_files_two_workers(tmp_path, oracle):
+    """three lane files on two GPU-reader workers.  A worker claims
+    its next file (and pins its first window) when it opens one; a worker
+    left with nothing to claim takes another worker's claimed-but-unstarted
+    file.  Every file is scored exactly once, with the oracle's sums."""
+    from mini_parallel_amd.synthetic import write_wgs_dataset
+    ds = write_wgs_dataset(str(tmp_path / "wgs"), lanes=3, reads_per_lane=1, reads_per_file=3000, bgzf=True,
+                           workers=3)
+    env = {"WGS_DATA_DIR": str(tmp_path / "wgs"), "WGS_SAMPLE_ID": "SYN", "WGS_LANES": "3",
+           "WGS_READS_PER_LANE": "1", "GPU_CHUNK_SIZE_READS": "1000", "WGS_RUN_ID": "three", "MSW_DEVICES": "0,0",
+           "MSW_GPU_INFLATE": "1"}
+    args = ["--full-wgs", "--gpu", "--score-mode", "sw", "--reference", ds["reference"], "--window", "300",
+            "--num-gpus", "2", "--checkpoint-dir", str(tmp_path), "--json", str(tmp_path / "rec.json")]
+    r = run(args, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    per_file = [int(oracle.sw_batch(b.reads, b.read_len, b.wins, b.win_len, threads=16)[0].astype(np.int64).sum())
+                for b in ds["batches"]]
+    rec = json.load(open(tmp_path / "rec.json"))
+    assert rec["files_processed"] == 3 and rec["total_reads"] == 3 * 3000 and rec["total_score"] == sum(per_file)
+    assert r.stdout.count("Processing file") == 3
+    ck = json.load(open(tmp_path / "checkpoint_three.json"))
+    assert [f["score"] for f in sorted(ck["files"], key=lambda f: f["file_index"])] == per_file
+
+
+@pytest.mark.gpu
 def test_full_wgs_file_shards(tmp_path, oracle):
     """WGS_FILE_SHARD=r/N (bench.py's config-4 leg: one process per GPU, rank
     r takes lane files r, r + N, ...): the two shards of a 2-way split cover

@@ -48,7 +48,7 @@ def layout(request, monkeypatch):
     length bucket on its own, and a forced G that cannot hold the batch's reads
     (KR > 24, or the LDS budget) falls back to G = 16.  Forced G = 8 / 9 on
     the 150 bp batches runs 19 / 17 packed rows per lane, the narrow groups
-    the model picks for batches of >= 48 waves per SIMD."""
+    the model picks for batches of >= 16 (G = 9) / 48 (G = 8) waves per SIMD."""
     if request.param == "auto":
         for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
             monkeypatch.delenv(k, raising=False)
@@ -129,6 +129,41 @@ def test_narrow_groups_large_batch(gpu_ctx, oracle, monkeypatch, capfd, sc):
     g = int(plan.split("G=")[1].split()[0])
     kr = int(plan.split("KR=")[1].split()[0])
     assert "layout=pairs" in plan and g in (8, 9) and 17 <= kr <= 19, line
+    s, i, j, _ = oracle.sw_batch_simd(b.reads, b.read_len, b.wins, b.win_len, match=sc.match, mismatch=sc.mismatch,
+                                      gap_open=sc.gap_open, gap_extend=sc.gap_extend, affine=sc.affine,
+                                      threads=THREADS, coords=sc.want_coords)
+    assert_same(got, (s, i, j), sc.want_coords)
+
+
+def _last_plan(capfd):
+    line = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")][-1]
+    plan = line.split("last_launch(")[1].split(")")[0]
+    return line, plan.split("layout=")[1].split()[0], int(plan.split("G=")[1].split()[0]), \
+        int(plan.split("KR=")[1].split()[0])
+
+
+@pytest.mark.parametrize("n", [131_072, 262_144, 524_288])
+@pytest.mark.parametrize("sc", [Scoring(), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)],
+                         ids=["linear", "affine_coords"])
+def test_narrow_gate_mid_batches(gpu_ctx, oracle, monkeypatch, capfd, sc, n):
+    """Config-3 batches (150 bp reads) either side of the measured narrow-group
+    crossover, each at the layout model's own choice: 9-lane groups of 17 rows
+    (14 pairs per wave) are taken from 16 waves per SIMD on (229k pairs on 256
+    CUs), 8-lane groups of 19 rows only from 48; below that the launch keeps
+    rows <= 16 per lane.  Every pair is checked against the SIMD oracle."""
+    for k in ("MSW_LAYOUT", "MSW_GROUP_LANES", "MSW_NO_MULTI"):
+        monkeypatch.delenv(k, raising=False)
+    simds = 4 * mpa.get_gpu_devices()[0].cu_count
+    b = config_batch(3, n_pairs=n, seed_offset=n % 977)
+    monkeypatch.setenv("MSW_HOST_TRACE", "1")
+    capfd.readouterr()
+    got = gpu_run(gpu_ctx, b, sc, chunk=n)
+    line, lay, g, kr = _last_plan(capfd)
+    if kr > 16:  # a narrow launch: only past its family's measured gate
+        per = 2 * (64 // g)
+        assert lay == "pairs" and -(-n // per) >= (16 if kr <= 17 else 48) * simds, line
+    if -(-n // 14) >= 16 * simds:  # past the 9-lane gate: the model takes it
+        assert kr > 16 and g in (8, 9), line
     s, i, j, _ = oracle.sw_batch_simd(b.reads, b.read_len, b.wins, b.win_len, match=sc.match, mismatch=sc.mismatch,
                                       gap_open=sc.gap_open, gap_extend=sc.gap_extend, affine=sc.affine,
                                       threads=THREADS, coords=sc.want_coords)

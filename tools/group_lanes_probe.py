@@ -24,7 +24,13 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--sizes", default="65536,131072,262144,1048576", help="pairs per launch, comma-separated")
+    ap.add_argument("--settings", default="auto,16", help="two MSW_GROUP_LANES settings to alternate ('auto' = model)")
+    ap.add_argument("--schemes", default="linear,linear_coords,affine_coords")
     a = ap.parse_args()
+    sizes = [int(x) for x in a.sizes.split(",")]
+    settings = a.settings.split(",")
+    schemes = a.schemes.split(",")
     import torch
     from mini_parallel_amd import Context
     from mini_parallel_amd.aligner import AFFINE, LINEAR, LINEAR_COORDS
@@ -33,13 +39,15 @@ def main():
     ctx = Context(0)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    for n in (65536, 131072, 262144, 1 << 20):
+    for n in sizes:
         b = config_shard(3, 0, n)  # 150 bp reads (indels: 149-151) x 300 bp windows
         t = lambda x, dt=None: torch.from_numpy(np.ascontiguousarray(x if dt is None else x.view(dt))).to(dev)  # noqa
         r, w, rl, wl = t(b.reads), t(b.wins), t(b.read_len, np.int16), t(b.win_len, np.int16)
         for name, sc in (("linear", LINEAR), ("linear_coords", LINEAR_COORDS), ("affine_coords", AFFINE)):
+            if name not in schemes:
+                continue
             ref = None
-            for g in ("auto", "16", "auto", "16", "auto", "16"):  # alternating: clocks drift under load
+            for g in settings * 3:  # alternating: clocks drift under load
                 if g == "auto":
                     os.environ.pop("MSW_GROUP_LANES", None)
                 else:
