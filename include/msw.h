@@ -221,7 +221,10 @@ void* msw_dev_alloc(msw_ctx* ctx, size_t bytes);
 void msw_dev_free(msw_ctx* ctx, void* p);
 int msw_memcpy_h2d(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
 int msw_memcpy_d2h(msw_ctx* ctx, void* dst, const void* src, size_t bytes);
-/* enqueued on `stream` (NULL = the context's compute stream); dst should be pinned */
+/* enqueued on `stream` (NULL = the context's compute stream); dst should be
+ * pinned: into pinned memory the copy runs as a kernel on that stream (not a
+ * DMA on the process-wide copy-engine rings, where a copy waiting on one
+ * stream holds up the copies of others); pageable dst: hipMemcpyAsync. */
 int msw_memcpy_d2h_async(msw_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
 int msw_synchronize(msw_ctx* ctx);
 /* A host-waitable point in `stream`'s work (NULL = the context's compute

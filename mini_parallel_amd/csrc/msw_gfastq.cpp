@@ -191,15 +191,24 @@ struct Inflater {
         d_crc = nullptr;
         h_flag = nullptr;
     }
-    // upload cbytes of compressed data + the member table, inflate into out, check CRCs
+    // upload cbytes of compressed data + the member table, inflate into out,
+    // check CRCs.  in_place: the device address of h_comp's pinned pages --
+    // the kernel then reads the compressed bytes over PCIe as it decodes
+    // instead of waiting for a DMA of the whole span first.
     int run(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, uint8_t* out,
-            hipStream_t s) {
+            hipStream_t s, const uint8_t* in_place = nullptr) {
         int rc;
-        if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
         if ((rc = grow(&d_mem, &mem_cap, mem.size()))) return rc;
         if ((rc = grow(&d_status, &status_cap, mem.size()))) return rc;
-        if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
-        GZ_TRY(hipMemsetAsync(dc + cbytes, 0, kInPad, s));
+        const uint8_t* src = in_place;
+        size_t src_bytes = cbytes;
+        if (!src) {
+            if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
+            if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
+            GZ_TRY(hipMemsetAsync(dc + cbytes, 0, kInPad, s));
+            src = dc;
+            src_bytes = cbytes + kInPad;
+        }
         if (!mem.empty())
             GZ_TRY(hipMemcpyAsync(d_mem, mem.data(), mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
         GZ_TRY(hipMemsetAsync(d_flag, 0, 4, s));
@@ -217,7 +226,7 @@ struct Inflater {
         uint32_t* d_prof = nullptr;
         if (prof_on && n) GZ_TRY(hipMalloc((void**)&d_prof, (size_t)n * 64));
         if (d_prof) GZ_TRY(hipMemsetAsync(d_prof, 0, (size_t)n * 64, s));
-        GZ_TRY(msw::launch_gz_inflate(dc, d_mem, n, out, d_status, d_flag, s, d_prof));
+        GZ_TRY(msw::launch_gz_inflate(src, src_bytes, d_mem, n, out, d_status, d_flag, s, d_prof));
         if (timing) GZ_TRY(hipEventRecord(ev[1], s));
         if (d_prof) {
             std::vector<uint32_t> h((size_t)n * 16);
@@ -632,7 +641,24 @@ int next_span(msw_gfastq* g) {
     const size_t lead = g->mapped ? (size_t)(g->map_off - g->reg_lo) : 0;
     if (lead)
         for (msw::GzMember& m : g->mem) m.coff += lead;
-    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s))) return rc;
+    // A file's first span, when small (<= MSW_GZ_IN_PLACE_MB compressed, 64 by
+    // default: config 3's 46 MB lane files), is read by the inflate kernel in
+    // place from the pinned window: nothing of this file is in flight yet to
+    // hide its upload behind, and the DMA of the whole span (~0.8 ms per
+    // 46 MB, two lanes sharing the link) would come first.  Later spans and
+    // large ones are uploaded (their DMA overlaps the previous span's work,
+    // and PCIe reads at decode time would slow inflate on a saturated link).
+    const uint8_t* in_place = nullptr;
+    const char* eip = getenv("MSW_GZ_IN_PLACE_MB");  // per span: tests switch it between readers
+    const uint64_t in_place_max = (eip ? strtoull(eip, nullptr, 10) : 64ull) << 20;
+    if (g->mapped && g->reg_len && g->cur < 0 && used + lead <= in_place_max) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, (void*)(g->hc - lead), 0) == hipSuccess && dp)
+            in_place = (const uint8_t*)dp;
+        else
+            (void)hipGetLastError();
+    }
+    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s, in_place))) return rc;
     // 3. the previous span's unfinished line goes right in front
     const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
     if (carry > kCarry)

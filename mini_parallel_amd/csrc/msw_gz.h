@@ -47,8 +47,11 @@ struct GzCrcConsts {
 };
 
 // Inflate every member of a span (one wave per member); status[m] set for each.
+// cdata: the span's compressed bytes, 4-byte aligned, cbytes of them readable
+// (device memory, or pinned host memory read in place); the kernel clamps
+// every load to them, so no padding after the span is needed.
 // prof (MSW_GZ_PROFILE builds only, else ignored): 16 u32 counters per member
-hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint32_t n, uint8_t* out,
+hipError_t launch_gz_inflate(const uint8_t* cdata, size_t cbytes, const GzMember* members, uint32_t n, uint8_t* out,
                              uint32_t* status, uint32_t* any_error, hipStream_t stream, uint32_t* prof = nullptr);
 // CRC-32 of every member's output against its trailer (one wave per member).
 hipError_t launch_gz_crc(const uint8_t* out, const GzMember* members, uint32_t n, const GzCrcConsts* consts,

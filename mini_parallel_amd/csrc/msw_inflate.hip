@@ -288,6 +288,9 @@ __device__ __noinline__ void build_fast(uint32_t lim_ll, int32_t bas_ll, uint32_
 // the decode, and nothing in the symbol loop waits on memory.
 struct Bits {
     const uint32_t* src;  // the span's compressed buffer as dwords
+    uint32_t last;        // its last readable dword: every load is clamped to it
+                          // (a buffer read in place from pinned host memory
+                          // has no zero padding after the span)
     uint64_t bb;
     uint32_t bcnt;        // valid bits in bb
     uint32_t wi;          // dword index of the next dword to merge
@@ -295,10 +298,11 @@ struct Bits {
     uint32_t cur;         // per lane: src[wbase + lane]
     uint32_t wmax;        // refills past this dword index mean truncated data
 
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return src[min(i, last)]; }
     __device__ __forceinline__ void prime(uint64_t byte_pos) {
         const uint32_t w = (uint32_t)(byte_pos >> 2), sh = 8u * (uint32_t)(byte_pos & 3);
         wbase = w;
-        cur = src[w + lane_id()];
+        cur = ld(w + lane_id());
         bb = (uint64_t)((uint32_t)__builtin_amdgcn_readlane((int)cur, 0) >> sh);
         bcnt = 32u - sh;
         wi = w + 1;
@@ -309,7 +313,7 @@ struct Bits {
             if (wi > wmax) return false;
             if (wi - wbase >= 64) {
                 wbase = wi;
-                cur = src[wbase + lane_id()];
+                cur = ld(wbase + lane_id());
             }
             const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(wi - wbase));
             bb |= (uint64_t)d << bcnt;
@@ -326,7 +330,7 @@ struct Bits {
     __device__ __forceinline__ void refill_fast() {
         if (wi - wbase >= 64) {
             wbase = min(wi, wmax);
-            cur = src[wbase + lane_id()];
+            cur = ld(wbase + lane_id());
         }
         const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)((wi - wbase) & 63u));
         bb |= (uint64_t)d << bcnt;
@@ -374,7 +378,7 @@ constexpr int inflate_waves() {
 
 template <uint32_t RING>
 __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(const uint8_t* __restrict__ cdata,
-                                                        const GzMember* __restrict__ members, uint32_t n,
+                                                        uint32_t cdata_last, const GzMember* __restrict__ members, uint32_t n,
                                                         uint8_t* __restrict__ out, uint32_t* __restrict__ status,
                                                         uint32_t* __restrict__ any_error, uint32_t* __restrict__ prof) {
     constexpr uint32_t kRing = RING, kRingMask = RING - 1;
@@ -403,6 +407,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
 
         Bits br;
         br.src = (const uint32_t*)cdata;
+        br.last = cdata_last;
         br.wmax = (uint32_t)((mem.coff + mem.clen) >> 2) + 2u;
         br.prime(mem.coff);
 
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                         const uint32_t j = j0 + 4u * lane;
                         if (j < rest) {
                             const uint64_t q = p + j;
-                            const uint32_t lo = br.src[q >> 2], hi = br.src[(q >> 2) + 1];
+                            const uint32_t lo = br.ld((uint32_t)(q >> 2)), hi = br.ld((uint32_t)(q >> 2) + 1u);
                             const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(q & 3));
                             const uint32_t nb = min(4u, rest - j);
                             // opos already counts the earlier rounds (j0 bytes)
@@ -665,7 +670,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
 #endif
                     if (pw - br.wbase > 59u) {
                         br.wbase = pw;
-                        br.cur = br.src[pw + lane];
+                        br.cur = br.ld(pw + lane);
                     }
                     // lane L's stream bits from bit P + L: dwords j .. j + 2 of the
                     // window, j = (pb + L) / 32, fetched from `cur` across lanes
@@ -826,7 +831,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 GZP(4, 1);
                 if (pw - br.wbase > 62u) {
                     br.wbase = min(pw, br.wmax);
-                    br.cur = br.src[br.wbase + lane];
+                    br.cur = br.ld(br.wbase + lane);
                 }
                 {
                     const uint32_t q = pw - br.wbase;
@@ -1032,12 +1037,14 @@ __global__ __launch_bounds__(256) void gz_crc_kernel(const uint8_t* __restrict__
 
 }  // namespace
 
-hipError_t launch_gz_inflate(const uint8_t* cdata, const GzMember* members, uint32_t n, uint8_t* out,
+hipError_t launch_gz_inflate(const uint8_t* cdata, size_t cbytes, const GzMember* members, uint32_t n, uint8_t* out,
                              uint32_t* status, uint32_t* any_error, hipStream_t stream, uint32_t* prof) {
     if (n == 0) return hipSuccess;
+    if (cbytes == 0 || ((uintptr_t)cdata & 3) || (cbytes + 3) / 4 > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t last = (uint32_t)((cbytes + 3) / 4 - 1);
     // One wave per member; the 2 KiB output ring in LDS (kDefaultRingKb:
     // 1 KiB measured the same, 4 / 8 KiB slower -- DESIGN.md 4.7).
-    hipLaunchKernelGGL(gz_inflate_kernel<kDefaultRingKb * 1024>, dim3(n), dim3(64), 0, stream, cdata, members, n,
+    hipLaunchKernelGGL(gz_inflate_kernel<kDefaultRingKb * 1024>, dim3(n), dim3(64), 0, stream, cdata, last, members, n,
                        out, status, any_error, prof);
     return hipGetLastError();
 }

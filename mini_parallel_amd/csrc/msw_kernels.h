@@ -172,6 +172,9 @@ hipError_t launch_cut_windows_for_reads(const uint8_t* genome, uint64_t glen, co
 // dst[i] = src[inv[i]] for score (and end_i / end_j when non-null): pair
 // order restored from slot-ordered results (one thread per pair, coalesced
 // stores; the slot-ordered source is small enough to stay in L2).
+// bytes from device memory to pinned host memory (dst: its device address),
+// as a kernel on `stream` (msw_memcpy_d2h_async)
+hipError_t launch_d2h_copy(void* dst, const void* src, uint64_t bytes, hipStream_t stream);
 hipError_t launch_gather_results(const uint32_t* inv, const int32_t* src_score, const int16_t* src_i,
                                  const int16_t* src_j, int32_t* score, int16_t* end_i, int16_t* end_j, uint64_t n,
                                  hipStream_t stream);

@@ -5,6 +5,7 @@
 // over the msw_launch_*.hip translation units (pairs linear / pairs affine /
 // split / mixed / multi linear / multi affine) so hipcc builds them in
 // parallel.  launch_sw / launch_sw_multi below pick the unit and instance.
+#include <algorithm>
 #include "msw_device.h"
 #include "msw_launch.h"
 
@@ -102,6 +103,25 @@ __global__ __launch_bounds__(256) void gather_results_kernel(const uint32_t* __r
     if (end_i) {
         end_i[k] = src_i[s];
         end_j[k] = src_j[s];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Device -> pinned host copy on the caller's stream (msw_memcpy_d2h_async):
+// 16-byte vector loads and stores over the body when source and destination
+// share their alignment mod 16, bytes for the head and tail (or everything
+// when they do not).  Plain vector stores over PCIe.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void d2h_copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                       uint64_t bytes, uint64_t head, uint64_t body16) {
+    const uint64_t tid = (uint64_t)blockIdx.x * 256u + threadIdx.x, nth = (uint64_t)gridDim.x * 256u;
+    uint4* d4 = reinterpret_cast<uint4*>(dst + head);
+    const uint4* s4 = reinterpret_cast<const uint4*>(src + head);
+    for (uint64_t k = tid; k < body16; k += nth) d4[k] = s4[k];
+    const uint64_t tail0 = head + 16u * body16, rest = head + (bytes - tail0);
+    for (uint64_t i = tid; i < rest; i += nth) {
+        const uint64_t b = i < head ? i : tail0 + (i - head);
+        dst[b] = src[b];
     }
 }
 
@@ -210,6 +230,21 @@ hipError_t launch_gather_results(const uint32_t* inv, const int32_t* src_score, 
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gather_results_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, inv, src_score, src_i,
                        src_j, score, end_i, end_j, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_d2h_copy(void* dst, const void* src, uint64_t bytes, hipStream_t stream) {
+    if (bytes == 0) return hipSuccess;
+    const uintptr_t ad = (uintptr_t)dst, as = (uintptr_t)src;
+    uint64_t head = bytes, body16 = 0;
+    if ((ad & 15) == (as & 15)) {
+        head = std::min<uint64_t>(bytes, (16 - (ad & 15)) & 15);
+        body16 = (bytes - head) / 16;
+    }
+    const uint64_t work = std::max<uint64_t>(body16, head + (bytes - head - 16 * body16));
+    const uint64_t blocks = std::min<uint64_t>(1024, std::max<uint64_t>(1, (work + 255) / 256));
+    hipLaunchKernelGGL(d2h_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (uint8_t*)dst, (const uint8_t*)src,
+                       bytes, head, body16);
     return hipGetLastError();
 }
 

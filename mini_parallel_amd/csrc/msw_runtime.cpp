@@ -1884,7 +1884,23 @@ int msw_memcpy_d2h_async(msw_ctx* ctx, void* dst, const void* src, size_t bytes,
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
     int rc = set_device(ctx);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream ? (hipStream_t)stream : ctx->compute));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
+    // Into pinned host memory the copy is a kernel on the caller's stream,
+    // not a DMA: the copy engines serve every stream of the process from
+    // shared in-order rings, so a DMA that waits on its stream's scoring
+    // kernel holds up the copies other workers queued behind it (config 3
+    // from FASTQ: one worker's result copies 2 ms late, behind the other's
+    // next batch).  MSW_D2H_DMA=1 keeps the DMA.
+    static const bool dma = getenv("MSW_D2H_DMA") != nullptr;
+    if (!dma && bytes && pinned_cached(ctx, dst, bytes)) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, dst, 0) == hipSuccess && dp) {
+            HIP_TRY(msw::launch_d2h_copy(dp, src, bytes, st));
+            return MSW_OK;
+        }
+        (void)hipGetLastError();
+    }
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
     return MSW_OK;
 }
 

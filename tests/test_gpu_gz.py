@@ -216,15 +216,22 @@ def assert_reader_parity(ctx, path, **kw):
     return len(hl)
 
 
-@pytest.mark.parametrize("mode", ["map", "copy"])
+def _reader_mode(monkeypatch, mode):
+    monkeypatch.setenv("MSW_GZ_NO_MAP", "1" if mode == "copy" else "0")
+    monkeypatch.setenv("MSW_GZ_IN_PLACE_MB", "0" if mode == "map_upload" else "64")
+
+
+@pytest.mark.parametrize("mode", ["map", "map_upload", "copy"])
 @pytest.mark.parametrize("block", [0xFF00, 1000])
 @pytest.mark.parametrize("crlf", [False, True])
 def test_reader_matches_host_reader(gpu_ctx, tmp_path, monkeypatch, block, crlf, mode):
-    """mode "map": compressed bytes DMA'd straight from the file's mapping
-    (page-cache pages pinned in place, one window per span, uploads starting
-    at the page boundary below the span); "copy": preads into pinned staging
+    """mode "map": compressed bytes from the file's mapping (page-cache pages
+    pinned in place, one window per span starting at the page boundary below
+    the span), the file's first span read by the inflate kernel in place over
+    PCIe and later spans DMA'd; "map_upload": every span DMA'd
+    (MSW_GZ_IN_PLACE_MB=0); "copy": preads into pinned staging
     (MSW_GZ_NO_MAP=1)."""
-    monkeypatch.setenv("MSW_GZ_NO_MAP", "1" if mode == "copy" else "0")
+    _reader_mode(monkeypatch, mode)
     data = fastq_text(20_000, 21 + block % 7, crlf=crlf)  # ~7-8 MB: several 1 MiB spans, records straddle them
     p = tmp_path / "lane.fastq.gz"
     p.write_bytes(bgzf_compress(data, 6, block=block))
@@ -311,9 +318,12 @@ def test_reader_parallel_compressed_reads(gpu_ctx, tmp_path, monkeypatch, thread
     assert assert_reader_parity(gpu_ctx, str(p)) == 20_000
 
 
-@pytest.mark.parametrize("mode", ["map", "copy"])
+@pytest.mark.parametrize("mode", ["map", "map_upload", "copy"])
 def test_reader_edge_files(gpu_ctx, tmp_path, monkeypatch, mode):
-    monkeypatch.setenv("MSW_GZ_NO_MAP", "1" if mode == "copy" else "0")
+    """Tiny and odd files; in "map" mode each is one span read in place, so
+    the kernel's input loads (clamped to the span) end inside the file's last
+    page."""
+    _reader_mode(monkeypatch, mode)
     rng = np.random.default_rng(5)
     cases = {
         "empty": b"",

@@ -528,3 +528,32 @@ def test_ctx_prepare_then_score(gpu_ctx, oracle):
                Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)):
         gpu_ctx.prepare(sc)
         assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), sc.want_coords)
+
+
+@pytest.mark.parametrize("nbytes,src_off,dst_off", [(1, 0, 0), (15, 0, 0), (4096 * 3 + 7, 0, 0), (1 << 20, 0, 0),
+                                                    (100_003, 4, 4), (65_536, 3, 7), (262_144 * 2, 16, 0)])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_memcpy_d2h_async(gpu_ctx, nbytes, src_off, dst_off, pinned):
+    """msw_memcpy_d2h_async: into pinned memory a copy kernel on the stream
+    (vector body when source and destination share their alignment mod 16,
+    bytes otherwise), into pageable memory a DMA; both followed by a fence."""
+    import ctypes
+    from mini_parallel_amd._lib import check, lib
+    from mini_parallel_amd.aligner import pinned_empty
+    L = lib()
+    rng = np.random.default_rng(nbytes)
+    data = rng.integers(0, 256, nbytes + src_off, dtype=np.uint8)
+    d = L.msw_dev_alloc(gpu_ctx.handle, nbytes + src_off + 16)
+    assert d
+    try:
+        check(L.msw_memcpy_h2d(gpu_ctx.handle, d, data.ctypes.data, data.nbytes))
+        out = pinned_empty(nbytes + dst_off + 16, np.uint8) if pinned else np.zeros(nbytes + dst_off + 16, np.uint8)
+        out[:] = 0xA5
+        fence = ctypes.c_uint64()
+        check(L.msw_memcpy_d2h_async(gpu_ctx.handle, out.ctypes.data + dst_off, d + src_off, nbytes, None))
+        check(L.msw_fence_record(gpu_ctx.handle, None, ctypes.byref(fence)))
+        check(L.msw_fence_wait(gpu_ctx.handle, fence.value))
+        assert np.array_equal(out[dst_off:dst_off + nbytes], data[src_off:])
+        assert (out[:dst_off] == 0xA5).all() and (out[dst_off + nbytes:] == 0xA5).all()
+    finally:
+        L.msw_dev_free(gpu_ctx.handle, d)
