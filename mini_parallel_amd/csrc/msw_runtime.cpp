@@ -1148,10 +1148,22 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     uint64_t fused_chunks = 0;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
+    // A short first chunk starts the GPU early; with chunks of more than 64k
+    // pairs the chunks after it double up to `chunk`, so each chunk's upload
+    // hides under the kernel of the one before (a large chunk straight after
+    // a small one left the GPU idle while it uploaded) and the large ones
+    // still reach the narrow lane groups.  1M config-3 pairs
+    // from pinned memory, genome form (tools/h2h_sweep.py,
+    // profiles/r05/h2h/chunk_ramp.jsonl): 131k / 262k / 524k chunks 8.29 /
+    // 8.49 / 9.41-9.49 ms -> 7.99 / 7.97-8.02 / 8.26-8.56; at 32k the ramp's
+    // extra chunk cost 1 % (7.92 -> 8.01), so smaller chunks keep the old
+    // schedule.  MSW_CHUNK_RAMP=0: no ramp.
+    const char* e_ramp = getenv("MSW_CHUNK_RAMP");
+    const bool ramp = chunk > 65536 && !(e_ramp && e_ramp[0] == '0');
+    uint64_t next_chunk = n > chunk ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8) : chunk;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
-        // A short first chunk starts the GPU early; the rest overlap (2-deep).
-        const uint64_t this_chunk =
-            (c == 0 && n > chunk) ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8) : chunk;
+        const uint64_t this_chunk = next_chunk;
+        next_chunk = ramp ? std::min<uint64_t>(chunk, 2 * next_chunk) : chunk;
         cnt = std::min(this_chunk, n - first);
         // Slots alternate across calls too, so consecutive async calls overlap.
         const uint64_t seq = ctx->slot_seq++;

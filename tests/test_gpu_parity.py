@@ -557,3 +557,25 @@ def test_memcpy_d2h_async(gpu_ctx, nbytes, src_off, dst_off, pinned):
         assert (out[:dst_off] == 0xA5).all() and (out[dst_off + nbytes:] == 0xA5).all()
     finally:
         L.msw_dev_free(gpu_ctx.handle, d)
+
+
+@pytest.mark.parametrize("ramp", ["1", "0"])
+@pytest.mark.parametrize("chunk", [20_000, 65_536, 70_000])
+def test_chunk_ramp(gpu_ctx, oracle, monkeypatch, ramp, chunk):
+    """A multi-chunk call: a short first chunk, then (chunk_pairs > 64k)
+    chunks doubling up to chunk_pairs, or (MSW_CHUNK_RAMP=0, smaller chunks)
+    the rest full size -- 100k config-3 pairs, affine + best cell, pairs
+    arrays and genome form, every pair against the SIMD oracle."""
+    monkeypatch.setenv("MSW_CHUNK_RAMP", ramp)
+    b = config_batch(3, n_pairs=100_000, seed_offset=77)
+    sc = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)
+    want = oracle_run(oracle, b, sc)
+    assert_same(gpu_run(gpu_ctx, b, sc, chunk=chunk), want, True)
+    ws = b.wins.shape[1]
+    g = gpu_ctx.load_genome(np.ascontiguousarray(b.wins).reshape(-1))
+    try:
+        got = gpu_ctx.align_reads(g, b.reads, b.read_len, np.arange(b.n_pairs, dtype=np.int64) * ws, b.win_len,
+                                  scoring=sc, chunk_pairs=chunk)
+    finally:
+        g.close()
+    assert_same(got, want, True)
