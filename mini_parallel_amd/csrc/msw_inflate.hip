@@ -651,6 +651,13 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                 else copy_far(len, dist);
             };
             const uint32_t lit_shift6 = 6u + 8u * min(lane, 2u);
+            // lane l: ceil(4096 / l) (lane 0: 0).  A window lane's offset off
+            // < 64 into a match of distance d has off mod d = off - d * ((off *
+            // M) >> 12) with M = this value of lane min(d, 64) mod 64: exact for
+            // d < 64 (the estimate's error is below off / 4096 < 1 / d), and
+            // d >= 64 reads lane 0 (M = 0: off mod d = off).  Integer ops and
+            // one ds_bpermute instead of a float reciprocal and a 32-bit multiply.
+            const uint32_t rmag = lane ? (4096u + lane - 1u) / lane : 0u;
             const uint64_t cend = mem.coff + mem.clen;
             const uint32_t ew = (uint32_t)(cend >> 2), eb = 8u * (uint32_t)(cend & 3u);
             // stream position (dword, bit) of the bit reader: wi * 32 - bcnt
@@ -743,12 +750,12 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                             const uint32_t off = lane - to;
                             const bool lit = (ti & 0x40000000u) == 0;
                             const uint32_t d = ((ti >> 15) & 0x7FFFu) + 1u;
-                            // overlapping copies repeat the token's last d bytes
-                            const float rd = __builtin_amdgcn_rcpf((float)d);
-                            int32_t r = (int32_t)off - (int32_t)((uint32_t)((float)off * rd)) * (int32_t)d;
-                            r += r < 0 ? (int32_t)d : 0;
-                            r -= r >= (int32_t)d ? (int32_t)d : 0;
-                            const int32_t src = (int32_t)(to + (uint32_t)r) - (int32_t)d;  // window-relative source
+                            // overlapping copies repeat the token's last d bytes:
+                            // r = off mod d (see rmag; lane address wraps mod 64)
+                            const uint32_t m = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(d, 64u) << 2), (int)rmag);
+                            const uint32_t q = __umul24(off, m) >> 12;  // floor(off / d)
+                            // window-relative source: to + (off mod d) - d = lane - d (q + 1)
+                            const int32_t src = (int32_t)lane - __mul24((int32_t)(q + 1u), (int32_t)d);
                             const bool dep = !lit && src >= 0;
                             const bool far = !lit && src < -(int32_t)RING;
                             uint32_t val = lit ? (((ti >> 6) >> (8u * (off & 3u))) & 0xFFu)
