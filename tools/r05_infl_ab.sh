@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 5: inflate's overlap modulo by a magic multiply (ds_bpermute of a
-# per-lane reciprocal table) against the float-reciprocal build of the commit
-# before it (tools/_ab/infl_old/libmsw.so, same tree otherwise).  GPU gz
+# Round 5: an inflate kernel change against the build of the commit before
+# it (tools/_ab/infl_old/libmsw.so: the same tree with the previous
+# msw_inflate.hip, tools/build_variant.sh).  GPU gz
 # tests, inflate kernel times (MSW_GZ_TIMING), config 3 from FASTQ and
 # config 4, old and new alternating.   bash tools/r05_infl_ab.sh TAG
 set -euo pipefail
