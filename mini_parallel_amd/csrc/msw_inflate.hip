@@ -44,7 +44,10 @@
 namespace msw {
 namespace {
 
-constexpr int kDefaultRingKb = 2;  // best measured throughput (tools/inflate_bench.py, profiles/r02/gz)
+#ifndef MSW_GZ_RING_KB
+#define MSW_GZ_RING_KB 2
+#endif
+constexpr int kDefaultRingKb = MSW_GZ_RING_KB;  // 2: best measured throughput (tools/inflate_bench.py, profiles/r02/gz)
 
 // MSW_GZ_PROFILE builds (tools/build_variant.sh gzprof -DMSW_GZ_PROFILE=1):
 // per-member event counts and cycle stamps into prof[m * 16 ..].
@@ -761,10 +764,18 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                             uint32_t val = lit ? (((ti >> 6) >> (8u * (off & 3u))) & 0xFFu)
                                                : (uint32_t)ring[(opos + (uint32_t)src) & kRingMask];
                             if (__builtin_amdgcn_ballot_w64(far && lane < W)) {
+#if MSW_GZ_PROFILE
+                                const uint64_t t_far = __builtin_amdgcn_s_memtime();
+#endif
                                 __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the flush stores have landed
                                 const uint64_t q = mem.ooff + (uint64_t)(far ? opos + (uint32_t)src : 0u);
                                 const uint32_t w = coherent_load(out + (q & ~(uint64_t)3));
                                 if (far) val = (w >> (8u * (uint32_t)(q & 3))) & 0xFFu;
+#if MSW_GZ_PROFILE
+                                (void)__builtin_amdgcn_readfirstlane(val);  // the load has landed
+                                GZP(6, 1);
+                                GZP(10, (uint32_t)(__builtin_amdgcn_s_memtime() - t_far));
+#endif
                             }
                             // bytes made by an earlier lane of this window: follow
                             // the pointers (a resolved lane points to itself)

@@ -43,15 +43,21 @@ def host_windows(genome: np.ndarray, pos: np.ndarray, want: np.ndarray):
     return W, eff.astype(np.uint16)
 
 
-@pytest.fixture(autouse=True, params=["genome_windows", "cut_slab"])
+@pytest.fixture(autouse=True, params=["genome_windows", "cut_slab", "copy_back"])
 def window_source(request, monkeypatch):
-    """Every test of this module twice: the packed kernels reading each
-    window straight from the resident genome (the default), and the windows
-    first cut into a slab (MSW_GENOME_CUT=1, also the path of long pairs)."""
-    if request.param == "cut_slab":
-        monkeypatch.setenv("MSW_GENOME_CUT", "1")
-    else:
+    """Every test of this module three times: the packed kernels reading each
+    window straight from the resident genome (the default), the windows first
+    cut into a slab (MSW_GENOME_CUT=1, also the path of long pairs), and that
+    with one-chunk calls copying their results back instead of the kernels
+    storing them into the slot's mapped host block (MSW_NO_DIRECT_OUT=1)."""
+    if request.param == "genome_windows":
         monkeypatch.delenv("MSW_GENOME_CUT", raising=False)
+    else:
+        monkeypatch.setenv("MSW_GENOME_CUT", "1")
+    if request.param == "copy_back":
+        monkeypatch.setenv("MSW_NO_DIRECT_OUT", "1")
+    else:
+        monkeypatch.delenv("MSW_NO_DIRECT_OUT", raising=False)
     return request.param
 
 
@@ -183,7 +189,9 @@ def test_genome_uniform_chunks(gpu_ctx, oracle, sc, n, chunk, monkeypatch, capfd
     trace = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")]
     chunks = int(trace[-1].split("chunks=")[1].split()[0])
     genome_chunks = int(trace[-1].split("genome_chunks=")[1].split()[0])
-    if window_source == "cut_slab":
+    direct_out = int(trace[-1].split("direct(")[1].split("out=")[1].split(")")[0])
+    assert direct_out == (0 if window_source == "copy_back" or chunks > 1 else 1), trace[-1]
+    if window_source != "genome_windows":
         assert genome_chunks == 0, trace[-1]
     elif n == 10_000:  # the config-2 shape: one chunk, pairs layout (smaller chunks may take the split layout)
         assert genome_chunks == chunks == 1, trace[-1]
