@@ -483,3 +483,28 @@ def test_reader_on_the_default_stream(gpu_ctx, tmp_path):
             got_l.append(ln)
     assert np.array_equal(np.concatenate(got_l), hl) and np.array_equal(np.concatenate(got_s), hs)
     assert torch.isfinite(x).all()
+
+
+@pytest.mark.parametrize("residue", [0, 1, 2, 3, 4093])
+def test_reader_in_place_file_end_at_page_boundary(gpu_ctx, tmp_path, monkeypatch, residue):
+    """A lane file read in place (its one span inflated by the kernel straight
+    from the pinned page-cache pages) whose size is `residue` bytes past a
+    4 KiB page boundary: the kernel's input loads are clamped to the span's
+    last dword, which may straddle the file's end but never the page after
+    it.  The last member's header line is padded until the size fits."""
+    monkeypatch.setenv("MSW_GZ_NO_MAP", "0")
+    monkeypatch.setenv("MSW_GZ_IN_PLACE_MB", "64")
+    main = bgzf_compress(fastq_text(3000, 71), 6, eof_block=False)
+    eof = bgzf_compress(b"", 6)  # the EOF block alone
+    data = None
+    for pad in range(0, 8200):
+        rec = b"@pad" + b"x" * pad + b" pos=5\nACGTNACGT\n+\nIIIIIIIII\n"
+        blob = main + bgzf_compress(rec, 0, eof_block=False) + eof
+        if len(blob) % 4096 == residue % 4096 and len(blob) > 4096:
+            data = blob
+            break
+    assert data is not None
+    p = tmp_path / "edge.fastq.gz"
+    p.write_bytes(data)
+    assert os.path.getsize(p) % 4096 == residue % 4096
+    assert assert_reader_parity(gpu_ctx, str(p)) == 3001
