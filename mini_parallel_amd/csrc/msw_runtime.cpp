@@ -302,7 +302,10 @@ struct msw_ctx {
         size_t bytes = 0;
         bool pinned = false;
     };
-    PinnedRange pinned_ranges[4];
+    // 8: a --full-wgs worker's five result copies per batch plus a call's
+    // reads / windows stay cached
+    static constexpr unsigned kPinnedRanges = 8;
+    PinnedRange pinned_ranges[kPinnedRanges];
     unsigned pinned_next = 0;
     // compat buffers
     uint8_t *c_s1 = nullptr, *c_s2 = nullptr;
@@ -1086,7 +1089,7 @@ bool pinned_cached(msw_ctx* ctx, const void* p, size_t bytes) {
     for (const msw_ctx::PinnedRange& r : ctx->pinned_ranges)
         if (r.p == p && r.bytes == bytes && p) return r.pinned;
     const bool pinned = is_pinned(p, bytes);
-    ctx->pinned_ranges[ctx->pinned_next++ % 4] = {p, bytes, pinned};
+    ctx->pinned_ranges[ctx->pinned_next++ % msw_ctx::kPinnedRanges] = {p, bytes, pinned};
     return pinned;
 }
 
