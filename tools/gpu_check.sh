@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > "$OUT/gputest.log" 2>&1
 echo "gpu tests ok: $(tail -1 "$OUT/gputest.log")"
-timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 python3 bench.py --detail "$OUT/bench_detail.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench ok"
 # fewer GPUs than asked for must fail loudly (rc != 0), never print n_gpus 1
 if timeout -k 10 120 python3 bench.py --gpus 2 --steps 2 --warmup 1 > "$OUT/gpus2.out" 2>&1; then
@@ -19,6 +19,6 @@ if timeout -k 10 120 python3 bench.py --gpus 2 --steps 2 --warmup 1 > "$OUT/gpus
 fi
 echo "gpus2 refused as expected: $(tail -1 "$OUT/gpus2.out")"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c2" -o t --output-format csv -- \
-  python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-pcie --extra-configs none \
+  python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-pcie --extra-configs none --detail "$OUT/prof_detail.json" \
   > "$OUT/prof_c2.log" 2>&1
 echo "profile ok"
