@@ -1906,8 +1906,7 @@ int msw_memcpy_d2h_async(msw_ctx* ctx, void* dst, const void* src, size_t bytes,
     // kernel holds up the copies other workers queued behind it (config 3
     // from FASTQ: one worker's result copies 2 ms late, behind the other's
     // next batch).  MSW_D2H_DMA=1 keeps the DMA.
-    static const bool dma = getenv("MSW_D2H_DMA") != nullptr;
-    if (!dma && bytes && pinned_cached(ctx, dst, bytes)) {
+    if (bytes && !getenv("MSW_D2H_DMA") && pinned_cached(ctx, dst, bytes)) {
         void* dp = nullptr;
         if (hipHostGetDevicePointer(&dp, dst, 0) == hipSuccess && dp) {
             HIP_TRY(msw::launch_d2h_copy(dp, src, bytes, st));

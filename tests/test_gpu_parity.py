@@ -533,10 +533,16 @@ def test_ctx_prepare_then_score(gpu_ctx, oracle):
 @pytest.mark.parametrize("nbytes,src_off,dst_off", [(1, 0, 0), (15, 0, 0), (4096 * 3 + 7, 0, 0), (1 << 20, 0, 0),
                                                     (100_003, 4, 4), (65_536, 3, 7), (262_144 * 2, 16, 0)])
 @pytest.mark.parametrize("pinned", [True, False])
-def test_memcpy_d2h_async(gpu_ctx, nbytes, src_off, dst_off, pinned):
+@pytest.mark.parametrize("dma", [False, True])
+def test_memcpy_d2h_async(gpu_ctx, monkeypatch, nbytes, src_off, dst_off, pinned, dma):
     """msw_memcpy_d2h_async: into pinned memory a copy kernel on the stream
     (vector body when source and destination share their alignment mod 16,
-    bytes otherwise), into pageable memory a DMA; both followed by a fence."""
+    bytes otherwise) or, with MSW_D2H_DMA=1, a DMA; into pageable memory a
+    DMA; all followed by a fence."""
+    if dma:
+        monkeypatch.setenv("MSW_D2H_DMA", "1")
+    else:
+        monkeypatch.delenv("MSW_D2H_DMA", raising=False)
     import ctypes
     from mini_parallel_amd._lib import check, lib
     from mini_parallel_amd.aligner import pinned_empty
