@@ -1133,12 +1133,11 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     const uint64_t chunk = chunk_pairs ? chunk_pairs : default_chunk();
     // A multi-chunk call pipelines its own chunks: copies on the copy stream,
     // kernels alternating between the two compute streams, results back on
-    // the d2h stream.  A one-chunk call keeps all of its work on one compute
-    // stream (no cross-stream events: ~5 HIP calls fewer per call, the host
-    // cost that bounds a stream of small async batches); async calls
-    // alternate that stream, so consecutive calls still overlap.  Its kernels
-    // store the results straight into the slot's mapped host block (no copy,
-    // no event after the kernels but the timing one).
+    // the d2h stream.  A one-chunk call keeps its kernels and results on one
+    // compute stream (async calls alternate it, so consecutive calls
+    // overlap; a synchronous call uploads there too) and its kernels store
+    // the results straight into the slot's mapped host block (no copy, no
+    // event after the kernels but the timing one).
     const bool multi_chunk = n > chunk;
     const bool alternate = multi_chunk || !sync;
     const bool direct_out = !multi_chunk && !getenv("MSW_NO_DIRECT_OUT");
@@ -1211,7 +1210,18 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         if (tr.on) tr.stage += tr.lap();
         // H2D on the copy stream, kernels on the compute stream (a one-chunk
         // call: everything on its compute stream).
-        hipStream_t up = multi_chunk ? ctx->copy : cs;
+        // Async calls upload on the copy stream (an event orders the kernel
+        // after it), so an upload never queues behind its compute stream's
+        // previous kernel.  All on one compute stream, async calls measured
+        // 54-148 us per 10k-pair batch depending on the box (105-148 on two
+        // of three: how the process's streams land on its hardware queues),
+        // with the separate upload 55-57 us on every box
+        // (profiles/r05/host/stream_ab*.jsonl).  MSW_ASYNC_ONE_STREAM=1:
+        // the one-stream form.  A synchronous one-chunk call keeps it (no
+        // other call in flight to overlap with).
+        const char* e_one = getenv("MSW_ASYNC_ONE_STREAM");
+        const bool sep_up = multi_chunk || (!sync && !(e_one && e_one[0] == '1'));
+        hipStream_t up = sep_up ? ctx->copy : cs;
         HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
         if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
         // [pos | rlen | wlen | order]: the contiguous part this chunk uses
@@ -1223,7 +1233,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         if (gmode && !fused)
             HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, b.genome->len, s.d_pos, s.d_wlen, s.d_wins, nullptr, ws,
                                             cnt, up));
-        if (multi_chunk) {
+        if (sep_up) {
             HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
             HIP_TRY(hipStreamWaitEvent(cs, s.uploaded, 0));
         }

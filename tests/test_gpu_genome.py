@@ -392,3 +392,33 @@ def test_error_paths(gpu_ctx):
     p = gpu_ctx.align_reads(g, R, np.array([4, 4], np.uint16), np.zeros(2, np.int64),
                             np.array([4, 4], np.uint16), asynchronous=True)
     assert list(p.wait()[0]) == [0, 0]  # zero reads vs ACGT: nothing matches byte 0
+
+
+@pytest.mark.parametrize("one_stream", ["0", "1"])
+def test_async_stream_upload_forms(gpu_ctx, oracle, monkeypatch, one_stream, window_source):
+    """A stream of one-chunk async calls (the host-to-host stream of bench.py,
+    three in flight, results waited oldest first and newest first): uploads
+    on the copy stream behind an event (default) or on the call's compute
+    stream (MSW_ASYNC_ONE_STREAM=1); every batch equals the oracle."""
+    monkeypatch.setenv("MSW_ASYNC_ONE_STREAM", one_stream)
+    rng = np.random.default_rng(17)
+    g = rng.choice(ACGT, 1_000_003)
+    n = 3_000
+    pos = rng.integers(0, g.size - 300, n).astype(np.int64)
+    rl = np.full(n, 150, np.uint16)
+    want = np.full(n, 300, np.uint16)
+    R = np.zeros((n, 160), np.uint8)
+    for k in range(n):
+        R[k, :150] = g[pos[k] + 70:pos[k] + 220]
+    genome = gpu_ctx.load_genome(g)
+    W, wl = host_windows(g, pos, want)
+    sc = SCHEMES[1]
+    expect = oracle_run(oracle, R, rl, W, wl, sc)
+    pend = []
+    for k in range(9):
+        pend.append(gpu_ctx.align_reads(genome, R, rl, pos, want, sc, asynchronous=True))
+        if len(pend) == 3:
+            assert_same(pend.pop(0).wait(), expect, sc.want_coords)
+    for p in pend[::-1]:
+        assert_same(p.wait(), expect, sc.want_coords)
+    genome.close()
