@@ -152,6 +152,11 @@ def parse(argv=None):
     ap.add_argument("--cpu-standin", action="store_true",
                     help="TEST ONLY (tests/test_bench_launcher.py): gloo ranks on the CPU with a "
                          "stand-in scorer, to exercise the launcher, sharding and gather without a GPU")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="TEST ONLY, oversubscribed: every rank runs the real GPU path on device 0 (contexts, "
+                         "kernels, per-rank CLI children with MSW_DEVICES=0), collectives over gloo on host "
+                         "tensors (RCCL refuses two ranks on one device); the line says \"oversubscribed\": "
+                         "true and is never a scaling point (tests/test_bench_contract.py)")
     return ap.parse_args(argv)
 
 
@@ -216,7 +221,7 @@ def launch_ranks(args, argv) -> int:
     n = args.gpus
     if not args.cpu_standin:
         have = visible_gpus()
-        if have < n:
+        if have < (1 if args.share_gpu else n):
             print(f"bench.py: --gpus {n} asked for {n} ranks but only {have} GPU(s) are visible; "
                   f"refusing to report a smaller run", file=sys.stderr, flush=True)
             return 3
@@ -524,11 +529,15 @@ class GpuWorkload:
 class Job:
     """This rank's place in the job and the bracket every timed region uses:
     synchronize, barrier, synchronize (the contract's form), max / sum over
-    ranks.  gpu=False is --cpu-standin (gloo, CPU tensors)."""
+    ranks.  gpu=False is --cpu-standin (gloo, CPU tensors).  shared=True is
+    --share-gpu: the GPU path on device 0 for every rank, collectives over
+    gloo on host tensors (comm_dev None)."""
 
-    def __init__(self, rank, world, local_rank, gpu, dev=None, stream=None):
+    def __init__(self, rank, world, local_rank, gpu, dev=None, stream=None, shared=False):
         self.rank, self.world, self.local_rank, self.gpu = rank, world, local_rank, gpu
-        self.dev, self.stream = dev, stream
+        self.dev, self.stream, self.shared = dev, stream, shared
+        self.dev_index = 0 if shared else local_rank  # the GPU this rank (and its CLI child) runs on
+        self.comm_dev = dev if (gpu and not shared) else None
 
     def sync(self):
         if self.gpu:
@@ -574,16 +583,25 @@ class Job:
 
     def max(self, vals):
         from mini_parallel_amd import dist as mdist
-        return mdist.max_over_ranks(vals, device=self.dev)
+        return mdist.max_over_ranks(vals, device=self.comm_dev)
 
     def sum(self, vals):
         from mini_parallel_amd import dist as mdist
-        return mdist.sum_over_ranks(vals, device=self.dev)
+        return mdist.sum_over_ranks(vals, device=self.comm_dev)
 
     def tensor(self, a):
         import torch
         t = torch.from_numpy(np.ascontiguousarray(a))
-        return t.to(self.dev) if self.gpu else t
+        return t.to(self.comm_dev) if self.comm_dev is not None else t
+
+    def wire(self, *ts):
+        """Result tensors as the process group moves them: on the GPU for
+        RCCL, copied to host memory for gloo (--share-gpu)."""
+        return [t if self.comm_dev is not None else t.cpu() for t in ts]
+
+    def gather(self, *ts):
+        from mini_parallel_amd import dist as mdist
+        return mdist.gather_results(*self.wire(*ts))
 
 
 def leg_pairs(job, ctx, cfg, args):
@@ -632,7 +650,7 @@ def leg_pairs(job, ctx, cfg, args):
         outs = [torch.from_numpy(s)]
     wall_max, kern_max = job.max([wall, kern])
     (job_cells,) = job.sum([batch.cells])
-    gathered = mdist.gather_results(*outs)
+    gathered = job.gather(*outs)
     if cfg == 3 and job.gpu and not args.no_h2h:
         dev_res = [t.cpu().numpy() for t in outs]
         del w, outs
@@ -1067,16 +1085,18 @@ def run_wgs_child(job, d, lanes, rpl, reference, extra_args, tag, timeout_s):
     wd = tempfile.mkdtemp(prefix=f"msw_{tag}_r{job.rank}_")
     env = dict(os.environ, WGS_DATA_DIR=d, WGS_SAMPLE_ID="SYN", WGS_LANES=str(lanes),
                WGS_READS_PER_LANE=str(rpl), GPU_CHUNK_SIZE_READS="65536",
-               WGS_FILE_SHARD=f"{job.rank}/{job.world}", MSW_DEVICES=str(job.local_rank),
+               WGS_FILE_SHARD=f"{job.rank}/{job.world}", MSW_DEVICES=str(job.dev_index),
                WGS_RUN_ID=f"bench_{tag}_r{job.rank}_{os.getpid()}")
     rec_path = os.path.join(wd, "rec.json")
     cmd = [cli, "--full-wgs", "--gpu", "--score-mode", "sw", "--reference", reference, "--window", str(C4_WINDOW),
            "--checkpoint-dir", wd, "--json", rec_path, "--num-gpus", "1"] + [x.replace("{wd}", wd) for x in extra_args]
     job.fence()
     t0 = time.perf_counter()
+    t_launch = time.time_ns()
     err, rec, ck = "", None, None
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+        t_end = time.time_ns()
         if r.returncode != 0:
             err = f"rustseq_mini exit {r.returncode}:\n" + (r.stdout[-1500:] + r.stderr[-1500:]).strip()
     except subprocess.TimeoutExpired as e:
@@ -1089,6 +1109,11 @@ def run_wgs_child(job, d, lanes, rpl, reference, extra_args, tag, timeout_s):
                 rec = json.load(f)
             with open(os.path.join(wd, f"checkpoint_{rec['run_id']}.json")) as f:
                 ck = json.load(f)
+            # the child's own timeline (CLOCK_REALTIME stamps in its record)
+            tm, tr = rec.get("t_main_unix_ns"), rec.get("t_record_unix_ns")
+            rec["process_phases"] = {"start_ms": (tm - t_launch) * 1e-6 if tm else 0.0,
+                                     "main_to_record_ms": (tr - tm) * 1e-6 if tm and tr else 0.0,
+                                     "exit_ms": (t_end - tr) * 1e-6 if tr else 0.0}
         except (OSError, ValueError, KeyError) as e:
             err = f"run record unreadable: {e}"
     if err:
@@ -1096,10 +1121,27 @@ def run_wgs_child(job, d, lanes, rpl, reference, extra_args, tag, timeout_s):
     return rec, ck, proc, wd, err
 
 
+def _files_by_rank(fi, rank, dev, world):
+    """The lane files each rank's CLI child processed (sorted) and the GPU
+    ordinal it ran on (MSW_DEVICES; -1 for the CPU stand-in), from the
+    gathered per-file rows."""
+    by = [sorted(int(f) for f, r in zip(fi, rank) if r == k) for k in range(world)]
+    devs = [sorted({int(d) for d, r in zip(dev, rank) if r == k}) for k in range(world)]
+    return by, [d[0] if len(d) == 1 else d for d in devs]
+
+
 def _setup_split(rec):
-    """The CLI's setup phases (max over its workers) as a flat list."""
+    """The CLI's setup phases (max over its workers), then its process
+    phases (PROCESS_PHASES), as a flat list."""
     ph = (rec or {}).get("setup_phases") or {}
-    return [float(ph.get(k, 0.0)) for k in SETUP_PHASES]
+    pp = (rec or {}).get("process_phases") or {}
+    return [float(ph.get(k, 0.0)) for k in SETUP_PHASES] + [float(pp.get(k, 0.0)) for k in PROCESS_PHASES]
+
+
+# the CLI child's process wall, split: exec -> main (dynamic loading of the
+# HIP runtime and libmsw), main -> run record written (HIP init, setup, the
+# timed work, teardown), record -> reaped by the parent (process exit)
+PROCESS_PHASES = ("start_ms", "main_to_record_ms", "exit_ms")
 
 
 SETUP_PHASES = ("hip_init_ms", "reference_load_ms", "context_ms", "genome_ms", "result_sets_ms", "lane_reader_ms",
@@ -1141,14 +1183,14 @@ def leg_config4(job, args):
     F, R = len(files), args.c4_reads_per_file
     mine = list(range(job.rank, F, job.world))
     rows, stats, err, cells = [], [0.0] * 5, "", 0
-    setup = [0.0] * len(SETUP_PHASES)
+    setup = [0.0] * (len(SETUP_PHASES) + len(PROCESS_PHASES))
     if job.gpu:
         rec, ck, proc, _, err = run_wgs_child(job, d, C4_LANES, C4_READS_PER_LANE, os.path.join(d, "reference.fa"),
                                               [], "c4", 900)
         if not err:
             for fr in ck["files"]:
                 rows.append([files.index(fr["file_path"]), fr["score"], fr["total_reads"], fr["total_bases"],
-                             1 if fr["completed"] else 0])
+                             1 if fr["completed"] else 0, job.rank, job.dev_index])
             stats = [rec["wall_ms"], proc * 1e3, rec["setup_ms"], rec["teardown_ms"], rec["kernel_ms"]]
             cells = int(rec["cells"])
             setup = _setup_split(rec)
@@ -1156,7 +1198,7 @@ def leg_config4(job, args):
         job.fence()
         t0 = time.perf_counter()
         for fi in mine:
-            rows.append([fi, *_standin_file(files[fi]), 1])
+            rows.append([fi, *_standin_file(files[fi]), 1, job.rank, -1])
         proc = time.perf_counter() - t0
         job.fence()
         stats = [proc * 1e3, proc * 1e3, 0.0, 0.0, 0.0]
@@ -1167,13 +1209,13 @@ def leg_config4(job, args):
     (g,) = mdist.gather_results(job.tensor(flat))
     if job.rank != 0:
         return None
-    g = g.cpu().numpy().reshape(-1, 5)
+    g = g.cpu().numpy().reshape(-1, 7)
     if tot[1]:
         return {"error": "the config-4 leg failed on some rank (see stderr)", "n_ranks": job.world,
                 "parity": {"bit_exact": False}}
     table = np.zeros((F, 4), np.int64)
     seen = np.zeros(F, np.int64)
-    for fi, sc, nr, nb, done in g:
+    for fi, sc, nr, nb, done, _, _ in g:
         table[fi] = (sc, nr, nb, done)
         seen[fi] += 1
     reads = int(table[:, 1].sum())
@@ -1186,7 +1228,10 @@ def leg_config4(job, args):
         ok_sc = (table[fi, 0] == e["score"]) if job.gpu else True
         if not (ok_rb and ok_sc and table[fi, 3] == 1 and seen[fi] == 1):
             bad.append(os.path.basename(p))
+    by_rank, dev_by_rank = _files_by_rank(g[:, 0], g[:, 5], g[:, 6], job.world)
     par = {"files": F, "files_once": bool((seen == 1).all()), "files_done": int(table[:, 3].sum()),
+           "files_by_rank": by_rank, "child_device_by_rank": dev_by_rank,
+           "files_sharded_as_cli": by_rank == [list(range(r, F, job.world)) for r in range(job.world)],
            "reads": reads, "reads_expected": F * R, "files_checked": F, "files_mismatched": bad,
            "check": "every lane file's (score i64, reads, bases) against the sums of its segments' oracle "
                     "results (oracle/sw_simd.c, each segment scored once when the pool was generated)"}
@@ -1212,6 +1257,7 @@ def leg_config4(job, args):
            "wall_ms": round(wall_ms, 1), "setup_ms": round(setup_ms, 1), "teardown_ms": round(tear_ms, 1),
            "process_wall_ms": round(proc_ms, 1), "max_kernel_ms": round(kern_ms, 1),
            "setup_phases_ms": {k: round(v, 1) for k, v in zip(SETUP_PHASES, mx[6:])},
+           "process_phases_ms": {k: round(v, 1) for k, v in zip(PROCESS_PHASES, mx[6 + len(SETUP_PHASES):])},
            "setup_bound_by": _setup_bound(dict(zip(SETUP_PHASES, mx[6:]))),
            "timing": "wall_ms = the --full-wgs driver's timed region (workers set up -> last results on the "
                      "host), max over ranks; setup_ms = contexts, genome upload and reader buffers before it "
@@ -1276,7 +1322,7 @@ def leg_config3_fastq(job, args):
     d, files, per = c3f_layout(args, job.world)
     F = len(files)
     stats, err, cells, recs, idx = [0.0] * 5, "", 0, [], []
-    setup = [0.0] * len(SETUP_PHASES)
+    setup = [0.0] * (len(SETUP_PHASES) + len(PROCESS_PHASES))
     if job.gpu:
         rec, ck, proc, wd, err = run_wgs_child(job, d, job.world, C3F_RPL, os.path.join(d, "reference.fa"),
                                                ["--gap-model", "affine", "--scores-out", "{wd}"], "c3f", 600)
@@ -1286,7 +1332,7 @@ def leg_config3_fastq(job, args):
                 raw = np.fromfile(os.path.join(wd, os.path.basename(fr["file_path"]) + ".scores"), np.uint8)
                 r = raw.view([("s", "<i4"), ("i", "<i2"), ("j", "<i2")])
                 recs.append(np.stack([r["s"].astype(np.int32), r["i"].astype(np.int32), r["j"].astype(np.int32)], 1))
-                idx.append([fi, r.shape[0], 1 if fr["completed"] else 0])
+                idx.append([fi, r.shape[0], 1 if fr["completed"] else 0, job.rank, job.dev_index])
             stats = [rec["wall_ms"], proc * 1e3, rec["setup_ms"], rec["teardown_ms"], rec["kernel_ms"]]
             cells = int(rec["cells"])
             setup = _setup_split(rec)
@@ -1296,7 +1342,7 @@ def leg_config3_fastq(job, args):
         for fi in range(job.rank, F, job.world):
             r = _standin_records(files[fi])
             recs.append(r)
-            idx.append([fi, r.shape[0], 1])
+            idx.append([fi, r.shape[0], 1, job.rank, -1])
         proc = time.perf_counter() - t0
         job.fence()
         stats = [proc * 1e3] * 2 + [0.0] * 3
@@ -1307,16 +1353,17 @@ def leg_config3_fastq(job, args):
     t_s, t_i, t_j = (job.tensor(np.ascontiguousarray(allr[:, c])) for c in range(3))
     # int16 coordinates ride the gather's int32 wire cast; the per-file index
     # rows (a different length) are a gather of their own
-    g_s, g_i, g_j = mdist.gather_results(t_s, t_i.to(dtype=_torch().int16), t_j.to(dtype=_torch().int16))
+    g_s, g_i, g_j = job.gather(t_s, t_i.to(dtype=_torch().int16), t_j.to(dtype=_torch().int16))
     (g_idx,) = mdist.gather_results(job.tensor(np.array(idx, np.int64).reshape(-1)))
     if job.rank != 0:
         return None
     if tot[1]:
         return {"error": "the config-3 FASTQ leg failed on some rank (see stderr)", "parity": {"bit_exact": False}}
     g_s, g_i, g_j = g_s.cpu().numpy(), g_i.cpu().numpy(), g_j.cpu().numpy()
-    g_idx = g_idx.cpu().numpy().reshape(-1, 3)
+    g_idx = g_idx.cpu().numpy().reshape(-1, 5)
+    by_rank, dev_by_rank = _files_by_rank(g_idx[:, 0], g_idx[:, 3], g_idx[:, 4], job.world)
     off, order = 0, {}
-    for fi, n, done in g_idx:
+    for fi, n, done, _, _ in g_idx:
         order[int(fi)] = (off, int(n), int(done))
         off += int(n)
     mism, checked, files_ok = 0, 0, 0
@@ -1348,10 +1395,13 @@ def leg_config3_fastq(job, args):
             "reads_per_s_incl_setup": round(reads / (setup_wall_ms * 1e-3)),
             "wall_ms": round(wall_ms, 1), "setup_ms": round(setup_ms, 1), "process_wall_ms": round(proc_ms, 1),
             "max_kernel_ms": round(kern_ms, 1),
+            "teardown_ms": round(tear_ms, 1),
             "setup_phases_ms": {k: round(v, 1) for k, v in zip(SETUP_PHASES, mx[6:])},
+            "process_phases_ms": {k: round(v, 1) for k, v in zip(PROCESS_PHASES, mx[6 + len(SETUP_PHASES):])},
             "setup_bound_by": _setup_bound(dict(zip(SETUP_PHASES, mx[6:]))),
             "parity": {"records_checked": checked, "records_expected": F * per, "mismatches": mism,
-                       "files_done": files_ok,
+                       "files_done": files_ok, "files_by_rank": by_rank, "child_device_by_rank": dev_by_rank,
+                       "files_sharded_as_cli": by_rank == [list(range(r, F, job.world)) for r in range(job.world)],
                        "bit_exact": mism == 0 and checked == F * per and files_ok == F,
                        "check": "every read's (score, end_i, end_j) against the oracle (oracle/sw_simd.c, "
                                 "affine + best cell), records gathered over the process group",
@@ -1393,7 +1443,7 @@ def main(argv=None):
     else:
         world = args.gpus or 1
         if world > 1:
-            if args.cpu_standin or visible_gpus() >= world:
+            if args.cpu_standin or visible_gpus() >= (1 if args.share_gpu else world):
                 prepare_datasets(args, extras, world)  # before the ranks start (they reuse it)
             return launch_ranks(args, argv)
     rank = int(os.environ.get("RANK", 0))
@@ -1414,26 +1464,28 @@ def main(argv=None):
     # device is what every barrier here means
     warnings.filterwarnings("ignore", message="barrier\\(\\): using the device under current context")
 
+    shared = gpu and args.share_gpu
+    dev_index = 0 if shared else local_rank
     if gpu:
         have = int(torch.cuda.device_count())
-        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-        if have < local_world or local_rank >= have:
-            print(f"bench.py: rank {rank} needs GPU {local_rank} of {local_world} but only {have} GPU(s) are visible",
+        local_world = 1 if shared else int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if have < local_world or dev_index >= have:
+            print(f"bench.py: rank {rank} needs GPU {dev_index} of {local_world} but only {have} GPU(s) are visible",
                   file=sys.stderr, flush=True)
             return 3
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(dev_index)
     # A process group at every N, N = 1 included: the gathers, max / sum
     # reductions and barriers of every leg run through RCCL ("nccl") on the
-    # GPUs whatever the GPU count (gloo for --cpu-standin).
+    # GPUs whatever the GPU count (gloo for --cpu-standin and --share-gpu).
     pg_init = "env://" if "WORLD_SIZE" in os.environ else f"tcp://127.0.0.1:{_free_port()}"
-    dist.init_process_group("nccl" if gpu else "gloo", init_method=pg_init, rank=rank, world_size=world,
-                            timeout=datetime.timedelta(minutes=30))
+    dist.init_process_group("nccl" if gpu and not shared else "gloo", init_method=pg_init, rank=rank,
+                            world_size=world, timeout=datetime.timedelta(minutes=30))
     # Build the communicator now, not inside a leg, and keep RCCL's version
     # banner (printed on stdout at communicator creation) off the one-line
     # stdout contract.
     with _stdout_to_stderr():
         from mini_parallel_amd import dist as _md
-        _md.sum_over_ranks([0], device=torch.device("cuda", local_rank) if gpu else None)
+        _md.sum_over_ranks([0], device=torch.device("cuda", dev_index) if gpu and not shared else None)
     from mini_parallel_amd import dist as mdist
     from mini_parallel_amd.synthetic import config_shard
 
@@ -1448,9 +1500,9 @@ def main(argv=None):
 
     ctx = None
     if gpu:
-        dev = torch.device("cuda", local_rank)
+        dev = torch.device("cuda", dev_index)
         from mini_parallel_amd import Context
-        ctx = Context(local_rank)
+        ctx = Context(dev_index)
         # A dedicated (non-null) stream: the kernels and the timing events share
         # it; a second one, created beside it (HIP maps streams onto its
         # hardware queues as they are created), for pipelined_steps.
@@ -1465,7 +1517,7 @@ def main(argv=None):
 
         def step():
             holder["s"] = standin_scores(batch)
-    job = Job(rank, world, local_rank, gpu, dev, stream)
+    job = Job(rank, world, local_rank, gpu, dev, stream, shared=shared)
 
     for _ in range(args.warmup):
         step()
@@ -1497,7 +1549,7 @@ def main(argv=None):
     # Final score/coordinate gather over RCCL (outside the timed region): the
     # only collective of the path.  Concatenated in rank order = global order.
     if gpu:
-        g_score, g_i, g_j = mdist.gather_results(work.score, work.ei, work.ej)
+        g_score, g_i, g_j = job.gather(work.score, work.ei, work.ej)
     else:
         (g_score,) = mdist.gather_results(torch.from_numpy(holder["s"]))
         g_i = g_j = None
@@ -1597,11 +1649,16 @@ def main(argv=None):
                             "note": "every max / sum / gather / barrier of the run goes through this process "
                                     "group (RCCL = the nccl backend on ROCm), at N = 1 too"},
         }
+        if shared:
+            line["oversubscribed"] = True
+            line["oversubscribed_note"] = (f"--share-gpu: {world} ranks on ONE GPU (device 0), collectives over "
+                                           "gloo on host tensors -- a functional run of the N > 1 GPU code, "
+                                           "never a scaling point")
         if not gpu:
             line["standin"] = True
             line["standin_scores"] = g_score.tolist() if g_score.size <= 100_000 else None
         detail = write_detail(args, world, line)
-        print(json.dumps(compact_line(line, detail)), flush=True)
+        print(json.dumps(fit_line(compact_line(line, detail))), flush=True)
 
     dist.barrier()
     dist.destroy_process_group()
@@ -1676,6 +1733,17 @@ def _leg_pairs_summary(e):
                     "cpu_gcups", "valu_frac", "hbm_frac", "traffic_over_alg")}
 
 
+def _phases(leg):
+    """A FASTQ leg's setup and process phases, whole milliseconds, short keys
+    (the phase names without their _ms suffix)."""
+    out = {}
+    for key, short in (("setup_phases_ms", "setup_phases"), ("process_phases_ms", "process_phases")):
+        ph = leg.get(key)
+        if ph:
+            out[short] = {k[:-3]: round(v) for k, v in ph.items()}
+    return out
+
+
 def summarize_legs(full):
     """The per-leg `summary` of the one-line record: for each BASELINE config
     and host-path leg its rate with unit, whether it was bit-exact and how
@@ -1713,13 +1781,18 @@ def summarize_legs(full):
         if f:
             fp = f.get("parity") or {}
             s["c3_fastq"] = {**_pick(f, "reads_per_s", "gcups_end_to_end", "reads_per_s_incl_setup",
-                                     "gcups_incl_setup", "wall_ms", "setup_ms", "error"),
-                             "bit_exact": fp.get("bit_exact"), "checked": fp.get("records_checked")}
+                                     "gcups_incl_setup", "wall_ms", "setup_ms", "teardown_ms", "process_wall_ms",
+                                     "error"),
+                             **_phases(f),
+                             "bit_exact": fp.get("bit_exact"), "checked": fp.get("records_checked"),
+                             **_pick({"distinct_reads": (f.get("dataset") or {}).get("distinct_reads")},
+                                     "distinct_reads")}
     c4 = ex.get("config4")
     if c4:
         p4 = c4.get("parity") or {}
         s["c4"] = {**_pick(c4, "reads_per_s", "reads_per_s_incl_setup", "reads_per_s_process", "gcups", "reads",
-                           "wall_ms", "setup_ms", "error"),
+                           "wall_ms", "setup_ms", "teardown_ms", "process_wall_ms", "error"),
+                   **_phases(c4),
                    "bit_exact": p4.get("bit_exact"), "checked": p4.get("files_checked"), "checked_unit": "files",
                    **_pick({"cpu_gcups": (c4.get("cpu_baseline") or {}).get("value")}, "cpu_gcups")}
     pc = full.get("pcie_inclusive")
@@ -1773,9 +1846,44 @@ def compact_line(full, detail_path=None):
     if col:
         line["collectives"] = _pick(col, "backend", "world", "calls_rank0")
     line["detail"] = detail_path
-    for k in ("standin", "standin_scores"):  # --cpu-standin test runs only
+    for k in ("standin", "standin_scores", "oversubscribed"):  # --cpu-standin / --share-gpu test runs only
         if k in full:
             line[k] = full[k]
+    return line
+
+
+def fit_line(line):
+    """Enforce LINE_LIMIT at run time: if the line is over it,
+    drop the optional parts of the summary in turn (phase splits, error
+    prose, then the cpu_baseline sample text), never the contract's keys,
+    and say so on stderr.  The detail file keeps everything."""
+    def size():
+        return len(json.dumps(line).encode())
+    if size() <= LINE_LIMIT:
+        return line
+    start, dropped = size(), []
+    summ = line.get("summary") or {}
+    for key in ("process_phases", "setup_phases"):
+        for leg in summ.values():
+            if isinstance(leg, dict) and leg.pop(key, None) is not None and f"summary.*.{key}" not in dropped:
+                dropped.append(f"summary.*.{key}")
+        if size() <= LINE_LIMIT:
+            break
+    if size() > LINE_LIMIT:
+        for leg in summ.values():
+            if isinstance(leg, dict) and isinstance(leg.get("error"), str) and len(leg["error"]) > 60:
+                leg["error"] = leg["error"][:57] + "..."
+                dropped.append("summary.*.error (trimmed)")
+    if size() > LINE_LIMIT and isinstance(line.get("cpu_baseline"), dict):
+        line["cpu_baseline"]["sample"] = str(line["cpu_baseline"].get("sample", ""))[:60]
+        dropped.append("cpu_baseline.sample (trimmed)")
+    if size() > LINE_LIMIT:
+        for k in [k for k in summ if k not in ("c2", "units")]:
+            summ[k] = {kk: summ[k][kk] for kk in ("gcups", "reads_per_s", "bit_exact", "checked")
+                       if isinstance(summ[k], dict) and kk in summ[k]}
+        dropped.append("summary legs cut to rate + parity")
+    print(f"bench.py: the one-line record was {start} B > LINE_LIMIT {LINE_LIMIT}; now {size()} B after "
+          f"dropping {', '.join(dict.fromkeys(dropped))} (the detail file keeps them)", file=sys.stderr, flush=True)
     return line
 
 

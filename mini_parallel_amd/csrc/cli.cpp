@@ -232,10 +232,17 @@ std::vector<Device> get_gpu_devices() {
 
 struct Ctx {
     msw_ctx* h = nullptr;
+    // --full-wgs workers leave their context (and buffers) to the process
+    // exit: main ends the process with _exit once the run record and the
+    // checkpoint are written, so releasing them one by one (50-60 ms of
+    // unregisters and frees after the last results) is work the OS redoes
+    bool keep = false;
     explicit Ctx(int ordinal) {
         if (msw_ctx_create(ordinal, &h) != MSW_OK) die(std::string("GPU context error: ") + msw_last_error());
     }
-    ~Ctx() { msw_ctx_destroy(h); }
+    ~Ctx() {
+        if (!keep) msw_ctx_destroy(h);
+    }
 };
 
 // gpu_align (aligner.rs:410-532) through msw_align_compat.
@@ -784,10 +791,29 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 const auto ts0 = Clock::now();
                 Ctx ctx(devices[gi].ordinal);
                 const double t_ctx = ms_since(ts0);
+                const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
+                // Setup after the context runs on two threads: the genome
+                // upload (copy stream) and the scoring kernels' module loads
+                // on a helper, beside the lane reader's buffers and the result
+                // sets here (each ~15-40 ms; in sequence they were the bulk of
+                // setup_ms, profiles/r06/c3f/).
+                msw_genome* gen = nullptr;
+                double t_gen = 0, t_kl = 0;
+                std::thread helper([&]() {
+                    const auto th0 = Clock::now();
+                    const std::string& ref_seq = genome();
+                    if (msw_genome_create(ctx.h, (const uint8_t*)ref_seq.data(), ref_seq.size(), &gen) != MSW_OK)
+                        die(std::string("GPU genome upload error: ") + msw_last_error());
+                    t_gen = ms_since(th0);
+                    // the scoring kernels' modules, loaded now rather than at the first batch
+                    if (msw_ctx_prepare(ctx.h, &sc) != MSW_OK) die(std::string("GPU kernel load: ") + msw_last_error());
+                    t_kl = ms_since(th0) - t_gen;
+                });
+                const auto tr0 = Clock::now();
                 msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
                 if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
                     die(std::string("GPU lane reader: ") + msw_last_error());
-                const double t_rd = ms_since(ts0);
+                const double t_rd = ms_since(tr0);
                 const size_t kNone = ~(size_t)0;
                 size_t pending = kNone;
                 auto claim = [&]() -> size_t {
@@ -796,20 +822,11 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 };
                 // the first file: claimed now and opened / pinned on the
                 // reader's thread (msw_gfastq_prefetch) while this worker
-                // uploads the genome and allocates its result sets, so its
-                // first window is ready when the clock starts
+                // allocates its result sets and the helper uploads the
+                // genome, so its first window is ready when the clock starts
                 pending = claim();
                 if (pending != kNone) (void)msw_gfastq_prefetch(gr, st[pending]->path.c_str());
-                const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
-                msw_genome* gen = nullptr;
-                const std::string& ref_seq = genome();
-                if (msw_genome_create(ctx.h, (const uint8_t*)ref_seq.data(), ref_seq.size(), &gen) != MSW_OK)
-                    die(std::string("GPU genome upload error: ") + msw_last_error());
-                // the scoring kernels' modules, loaded now rather than at the first batch
-                const double t_kl0 = ms_since(ts0);
-                if (msw_ctx_prepare(ctx.h, &sc) != MSW_OK) die(std::string("GPU kernel load: ") + msw_last_error());
-                const double t_kl = ms_since(ts0) - t_kl0;
-                const double t_gen = ms_since(ts0);
+                const auto tres0 = Clock::now();
                 // two result sets: batch k's copy-back lands while batch k+1 runs
                 struct Res {
                     int32_t* d_score = nullptr;
@@ -831,6 +848,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     if (!r.d_score || !r.d_ei || !r.d_ej || !r.d_wlen || !r.h)
                         die(std::string("GPU lane reader buffers: ") + msw_last_error());
                 }
+                const double t_res = ms_since(tres0);
+                helper.join();
                 unsigned long long alg_local = 0;
                 // per file this worker has open: batches in flight, reader done
                 std::map<size_t, std::pair<int, bool>> open_files;
@@ -886,7 +905,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     trace_ev(wi, "settled", r.n);
                 };
                 int cur = 0;
-                setup_phase(t_ctx, t_gen - t_rd - t_kl, ms_since(ts0) - t_gen, t_rd - t_ctx, t_kl);
+                setup_phase(t_ctx, t_gen, t_res, t_rd, t_kl);
                 // the reader's stats of the file it just finished
                 auto reader_done = [&](size_t fi) {
                     uint64_t bi = 0, bo = 0;
@@ -997,17 +1016,13 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 settle(res[cur]);
                 settle(res[cur ^ 1]);
                 mark_done();
-                msw_gfastq_close(gr);
-                for (Res& r : res) {
-                    msw_dev_free(ctx.h, r.d_score);
-                    msw_dev_free(ctx.h, r.d_ei);
-                    msw_dev_free(ctx.h, r.d_ej);
-                    msw_dev_free(ctx.h, r.d_wlen);
-                    msw_host_free(r.h);
-                }
-                msw_genome_destroy(gen);
                 msw_ctx_stats(ctx.h, &gstats[(size_t)wi], 0);
                 gstats[(size_t)wi].alg_bytes = alg_local;
+                // the reader, result sets, genome and context stay allocated:
+                // the process exits (_exit in main) once the record is written
+                (void)gr;
+                (void)gen;
+                ctx.keep = true;
             });
         }
         gate.release_when(nworkers);
@@ -1252,8 +1267,9 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 pending.pop_front();
             }
             mark_done();
-            msw_genome_destroy(gen);
             msw_ctx_stats(ctx.h, &gstats[(size_t)g], 0);
+            (void)gen;  // left to the process exit, like the context (Ctx::keep)
+            ctx.keep = true;
         });
     }
     gate.release_when(ngpu);
@@ -1301,7 +1317,17 @@ void write_json(const std::string& path, const std::string& body) {
 
 }  // namespace
 
+// CLOCK_REALTIME in ns: the run record's process timeline (t_main_unix_ns,
+// t_record_unix_ns), so a parent can split its child's wall into start-up
+// (exec -> main), main -> record and exit (record -> reaped).
+long long unix_ns() {
+    timespec t;
+    clock_gettime(CLOCK_REALTIME, &t);
+    return (long long)t.tv_sec * 1000000000ll + t.tv_nsec;
+}
+
 int main(int argc, char** argv) {
+    const long long t_main_ns = unix_ns();
     load_dotenv();
     const Args a = parse_args(argc, argv);
     // --full-wgs sw: the reference loads beside the HIP runtime init
@@ -1448,9 +1474,15 @@ int main(int argc, char** argv) {
           << ", \"kernel_load_ms\": " << rep.kernel_load_ms << "}"
           << ", \"teardown_ms\": " << rep.teardown_ms
           << ", \"inflate_bytes_in\": " << rep.gz_in << ", \"inflate_bytes_out\": " << rep.gz_out
-          << ", \"reads_per_second\": " << reads / secs << "}\n";
+          << ", \"reads_per_second\": " << reads / secs << ", \"t_main_unix_ns\": " << t_main_ns
+          << ", \"t_record_unix_ns\": " << unix_ns() << "}\n";
         write_json(a.json, j.str());
-        return all_ok ? 0 : 1;
+        // Records, scores files and checkpoint are written and closed: end the
+        // process here.  The workers' contexts, genomes and pinned buffers are
+        // released by the exit itself (Ctx::keep), not call by call.
+        fflush(stdout);
+        fflush(stderr);
+        _exit(all_ok ? 0 : 1);
     }
 
     if (a.test_wgs) {

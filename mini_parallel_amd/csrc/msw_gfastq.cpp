@@ -44,6 +44,7 @@ namespace msw_detail {
 int set_error(int code, const char* fmt, ...);
 int ctx_device(const msw_ctx* c);
 hipStream_t ctx_compute_stream(const msw_ctx* c);
+uint64_t ctx_gz_group_bytes(const msw_ctx* c);
 }  // namespace msw_detail
 
 using msw_detail::set_error;
@@ -275,6 +276,10 @@ struct Inflater {
 struct msw_gfastq {
     msw_ctx* ctx = nullptr;
     int device = 0;
+    // the reader's switches, read once at msw_gfastq_open (tests set them per reader)
+    int read_threads = 4;              // MSW_GZ_READ_THREADS (1..8): threads of a large compressed top-up
+    uint64_t in_place_max = 64ull << 20;  // MSW_GZ_IN_PLACE_MB: first spans up to this are inflated in place
+    bool no_map = false;               // MSW_GZ_NO_MAP=1: copied mode (preads into pinned staging)
     hipStream_t rs = nullptr;          // the reader's own stream (inflate + parse)
     hipEvent_t parsed = nullptr;       // phase B of the current span done
     // per span buffer i (dout[i] and its line arrays pb[i]): the last emit
@@ -443,8 +448,8 @@ void release(msw_gfastq* g) {
 
 // Top up hc with compressed bytes from the file (up to want, within cap).
 // Positioned reads (pread at fread_off); a large top-up -- a new file's
-// first span, ~180 MB at the config-4 shape -- is split over 4 threads
-// (MSW_GZ_READ_THREADS, 1..8): one
+// first span, ~180 MB at the config-4 shape -- of 32 MiB or more is split
+// over 4 threads (MSW_GZ_READ_THREADS, 1..8): one
 // thread copies page-cache data into pinned memory at ~11 GB/s, and 16 ms of
 // it per file left the GPU idle between files (MSW_GFASTQ_TRACE).
 int fill_compressed(msw_gfastq* g, size_t want) {
@@ -462,12 +467,8 @@ int fill_compressed(msw_gfastq* g, size_t want) {
         }
         return true;
     };
-    // read per call (a few per file): tests change them between readers
-    const char* et = getenv("MSW_GZ_READ_THREADS");
-    const char* es = getenv("MSW_GZ_READ_SPLIT");  // smallest top-up split over threads (bytes)
-    const int threads = std::max(1, std::min(8, et ? atoi(et) : 4));
-    const uint64_t split = es && atoll(es) > 0 ? (uint64_t)atoll(es) : (32ull << 20);
-    const int parts = todo >= split ? threads : 1;
+    const int threads = g->read_threads;
+    const int parts = todo >= (32ull << 20) ? threads : 1;
     const uint64_t per = (todo + parts - 1) / parts;
     bool ok[8] = {true, true, true, true, true, true, true, true};
     std::vector<std::thread> th;
@@ -649,9 +650,7 @@ int next_span(msw_gfastq* g) {
     // large ones are uploaded (their DMA overlaps the previous span's work,
     // and PCIe reads at decode time would slow inflate on a saturated link).
     const uint8_t* in_place = nullptr;
-    const char* eip = getenv("MSW_GZ_IN_PLACE_MB");  // per span: tests switch it between readers
-    const uint64_t in_place_max = (eip ? strtoull(eip, nullptr, 10) : 64ull) << 20;
-    if (g->mapped && g->reg_len && g->cur < 0 && used + lead <= in_place_max) {
+    if (g->mapped && g->reg_len && g->cur < 0 && used + lead <= g->in_place_max) {
         void* dp = nullptr;
         if (hipHostGetDevicePointer(&dp, (void*)(g->hc - lead), 0) == hipSuccess && dp)
             in_place = (const uint8_t*)dp;
@@ -845,9 +844,7 @@ int open_file(msw_gfastq* g, const char* path) {
         GZ_TRY(hipSetDevice(g->device));
         GZ_TRY(hipMemcpyAsync(g->d_state, g->d_state0, sizeof(msw::ParseState), hipMemcpyDeviceToDevice, g->rs));
     }
-    const char* nm = getenv("MSW_GZ_NO_MAP");  // per file: tests switch it between readers
-    const bool no_map = nm && atoi(nm) != 0;
-    if (!no_map && g->fsize > 0) {
+    if (!g->no_map && g->fsize > 0) {
         void* m = mmap(nullptr, (size_t)g->fsize, PROT_READ, MAP_SHARED, fileno(g->f), 0);
         if (m != MAP_FAILED) {
             g->map = (uint8_t*)m;
@@ -892,6 +889,14 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     g->stride = read_stride;
     g->max_reads = max_reads;
     g->want_pos = want_pos != 0;
+    {
+        const char* et = getenv("MSW_GZ_READ_THREADS");
+        g->read_threads = std::max(1, std::min(8, et ? atoi(et) : 4));
+        const char* eip = getenv("MSW_GZ_IN_PLACE_MB");
+        if (eip) g->in_place_max = strtoull(eip, nullptr, 10) << 20;
+        const char* nm = getenv("MSW_GZ_NO_MAP");
+        g->no_map = nm && atoi(nm) != 0;
+    }
     if (span_bytes == 0) {
         const char* e = getenv("MSW_GFASTQ_SPAN_MB");
         span_bytes = e && atoll(e) > 0 ? (uint64_t)atoll(e) << 20 : kDefaultSpan;
@@ -939,8 +944,7 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     {
         // copied mode asked for up front: its pinned staging now, with the
         // other buffers (~85 ms per 512 MB), not at the first file's read
-        const char* nm = getenv("MSW_GZ_NO_MAP");
-        if (nm && atoi(nm) != 0 && (rc = ensure_stage(g))) return bail(rc);
+        if (g->no_map && (rc = ensure_stage(g))) return bail(rc);
     }
     const size_t ob = (size_t)(kCarry + g->span + kPad);
     for (int i = 0; i < 2; ++i) {
@@ -994,8 +998,7 @@ int msw_gfastq_reset(msw_gfastq* g, const char* path) {
 int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
     if (!g || !path) return set_error(MSW_E_INVALID, "reader/path is NULL");
     drop_prefetch(g);
-    const char* nm = getenv("MSW_GZ_NO_MAP");
-    if (nm && atoi(nm) != 0) return MSW_OK;  // copied mode: nothing to pin ahead
+    if (g->no_map) return MSW_OK;  // copied mode: nothing to pin ahead
     g->pf.path = path;
     const size_t cap = g->in_cap;
     const uint64_t span = g->span;
@@ -1104,8 +1107,9 @@ int msw_bgzf_inflate(msw_ctx* ctx, const uint8_t* data, uint64_t len, uint8_t* o
     int rc = inf.init();
     uint8_t* dout = nullptr;
     uint8_t* hstage = nullptr;
-    const char* ge = getenv("MSW_GZ_GROUP_MB");  // output bytes per launch (tools/inflate_bench.py)
-    const uint64_t kGroup = (ge && atoll(ge) > 0 ? (uint64_t)atoll(ge) : 1024u) << 20;  // ~16k members: two waves per SIMD slot
+    // output bytes per launch, MSW_GZ_GROUP_MB (default 1024: ~16k members,
+    // two waves per SIMD slot), read at context creation
+    const uint64_t kGroup = msw_detail::ctx_gz_group_bytes(ctx);
     const size_t kStage = (size_t)(kGroup + kGroup / 8 + (4u << 20));  // pinned staging: a group's compressed bytes
     uint64_t p = 0, total = 0;
     std::vector<msw::GzMember> mem;

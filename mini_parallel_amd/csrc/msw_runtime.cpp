@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <deque>
 #include <string>
 #include <unordered_map>
@@ -67,8 +68,61 @@ namespace {
 
 inline uint32_t dup16(uint32_t v) { return (v & 0xFFFFu) | ((v & 0xFFFFu) << 16); }
 
+// The library's run-time switches, read ONCE when a context is created
+// (msw_ctx_create -> read_options) and kept in the context: no call or launch
+// path reads the environment.  Every one forces a code path the tests cover
+// (INTEGRATION.md section 4), or turns a diagnostic trace on.
+struct Options {
+    bool no_f16 = false;          // MSW_NO_F16: the integer path for every launch
+    bool force_long = false;      // MSW_FORCE_LONG=1: every pair on the long-pair kernel
+    uint64_t long_blocks = 0;     // MSW_LONG_BLOCKS: a fixed long-pair block count (work-queue grids)
+    bool layout_set = false;      // MSW_LAYOUT given (per-bucket launches then)
+    bool force_pairs = false, force_split = false, force_mixed = false;  // its value
+    bool group_set = false;       // MSW_GROUP_LANES given
+    uint32_t group_lanes = 0;     // its value (8..16)
+    bool no_multi = false;        // MSW_NO_MULTI: one launch per bucket
+    bool host_trace = false;      // MSW_HOST_TRACE: per-call host phase times on stderr
+    std::string wave_trace;       // MSW_WAVE_TRACE=file: per-block placement records
+    uint64_t chunk = 65536;       // GPU_CHUNK_SIZE_READS: default pairs per staged chunk (aligner.rs:9-15)
+    uint64_t gz_group_bytes = 1024ull << 20;  // MSW_GZ_GROUP_MB: output bytes per msw_bgzf_inflate launch
+};
+
+Options read_options() {
+    Options o;
+    auto has = [](const char* k) { return getenv(k) != nullptr; };
+    o.no_f16 = has("MSW_NO_F16");
+    const char* fl = getenv("MSW_FORCE_LONG");
+    o.force_long = fl && *fl == '1';
+    const char* lb = getenv("MSW_LONG_BLOCKS");
+    o.long_blocks = lb && atoll(lb) > 0 ? (uint64_t)atoll(lb) : 0;
+    const char* lay = getenv("MSW_LAYOUT");
+    o.layout_set = lay != nullptr;
+    o.force_pairs = lay && !strcmp(lay, "pairs");
+    o.force_split = lay && !strcmp(lay, "split");
+    o.force_mixed = lay && !strcmp(lay, "mixed");
+    const char* g = getenv("MSW_GROUP_LANES");
+    o.group_set = g != nullptr;
+    o.group_lanes = g ? (uint32_t)atoi(g) : 0u;
+    o.no_multi = has("MSW_NO_MULTI");
+    o.host_trace = has("MSW_HOST_TRACE");
+    const char* wt = getenv("MSW_WAVE_TRACE");
+    o.wave_trace = wt ? wt : "";
+    const char* v = getenv("GPU_CHUNK_SIZE_READS");
+    if (v && *v) {
+        char* end = nullptr;
+        const unsigned long long n = strtoull(v, &end, 10);
+        if (end && *end == '\0' && n > 0) o.chunk = n;
+    }
+    const char* gz = getenv("MSW_GZ_GROUP_MB");
+    if (gz && atoll(gz) > 0) o.gz_group_bytes = (uint64_t)atoll(gz) << 20;
+    return o;
+}
+
+const Options kDefaultOptions{};
+
 // Validated kernel constants for one scoring scheme.
 struct Scheme {
+    const Options* opt = &kDefaultOptions;  // the context's switches
     bool affine, coords;
     uint32_t match2, delta2, gap2, open_ext2, bias2, code_shift;
     int32_t match;
@@ -79,8 +133,9 @@ struct Scheme {
     uint32_t f16_hi, f16_ngap2, f16_noe2;
 };
 
-int make_scheme(const msw_scoring_t* sc, Scheme* s) {
+int make_scheme(const msw_scoring_t* sc, const Options& opt, Scheme* s) {
     if (!sc) return fail(MSW_E_INVALID, "scoring is NULL");
+    s->opt = &opt;
     if (sc->match < 1 || sc->match > 64)
         return fail(MSW_E_RANGE, "match=%d outside [1, 64]", sc->match);
     if (sc->mismatch > 0 || sc->match - sc->mismatch > 64)
@@ -119,7 +174,7 @@ int make_scheme(const msw_scoring_t* sc, Scheme* s) {
 
 // The f16 path holds every cell value (<= match * min(m, n)) below 2048.
 bool f16_fits(const Scheme& s, uint32_t max_m, uint32_t max_n) {
-    if (getenv("MSW_NO_F16")) return false;  // tests: force the integer path
+    if (s.opt->no_f16) return false;  // tests: force the integer path
     return s.f16_scheme && (uint64_t)s.match * (std::min(max_m, max_n) + 2u) < 2048u;
 }
 
@@ -141,13 +196,8 @@ int check_bounds(const Scheme& s, uint32_t max_m, uint32_t max_n) {
 inline bool is_long(uint32_t m, uint32_t n) {
     return m > (uint32_t)msw::kMaxReadLen || n > (uint32_t)msw::kMaxWinLen;
 }
-// MSW_FORCE_LONG=1 sends every pair to the long-pair kernel (tests and
-// tools/long_bench.py run it on the packed kernels' shapes); read once per
-// call, like MSW_LAYOUT.
-inline bool force_long() {
-    const char* e = getenv("MSW_FORCE_LONG");
-    return e && *e == '1';
-}
+// MSW_FORCE_LONG=1 (Options::force_long) sends every pair to the long-pair
+// kernel (tests and tools/long_bench.py run it on the packed kernels' shapes).
 
 // Long-pair launch (p's pointers, order and output fields set by the caller):
 // one wave per pair, one block per slot: the dispatcher fills every wave slot
@@ -175,8 +225,7 @@ int launch_long(const Scheme& sch, msw::SwParams p, uint64_t n, uint32_t max_m, 
         blocks = (n + rounds - 1) / rounds;
     }
     blocks = std::min<uint64_t>(blocks, per_block ? std::max<uint64_t>(resident, (1ull << 30) / per_block) : 1ull << 20);
-    const char* env = getenv("MSW_LONG_BLOCKS");  // experiments: a fixed block count
-    if (env && atoll(env) > 0) blocks = std::min<uint64_t>(n, (uint64_t)atoll(env));
+    if (sch.opt->long_blocks) blocks = std::min<uint64_t>(n, sch.opt->long_blocks);  // tests: a fixed block count
     const bool queue = n > blocks;
     const size_t scratch_bytes = (size_t)blocks * per_block;
     uint8_t* mem = nullptr;
@@ -277,6 +326,11 @@ void free_slot(Slot& s) {
 struct msw_ctx {
     int device = 0;
     int cu_count = 256;
+    Options opt;  // the environment's switches, read at creation
+    // compute: created with the context; the others on first use
+    // (aux_streams): a stream costs 3-30 ms to create (the first few each make
+    // a hardware queue) and as much to destroy, and the --full-wgs workers
+    // and device-resident callers never use them (profiles/r06/c3f/)
     hipStream_t compute = nullptr, copy = nullptr, d2h = nullptr;
     // multi-chunk calls alternate their chunks' kernels over compute and
     // compute2, so chunk k+1's waves start under chunk k's tail (one stream
@@ -296,17 +350,20 @@ struct msw_ctx {
     // epoch_next is recorded, and once it has completed becomes the epoch)
     hipEvent_t epoch = nullptr, epoch_next = nullptr;
     double busy_until = 0.0;     // ms after epoch at which the counted scoring intervals end
-    // pinned_cached: the last few (address, bytes) ranges asked about
+    // pinned_cached: the most recently used (address, bytes) ranges asked
+    // about, most recent first (move to front on a hit).  16: a --full-wgs
+    // worker's two result sets x five copies per batch, plus a call's reads /
+    // windows, stay cached (the 8-entry FIFO missed every one).
     struct PinnedRange {
         const void* p = nullptr;
         size_t bytes = 0;
         bool pinned = false;
     };
-    // 8: a --full-wgs worker's five result copies per batch plus a call's
-    // reads / windows stay cached
-    static constexpr unsigned kPinnedRanges = 8;
+    static constexpr unsigned kPinnedRanges = 16;
     PinnedRange pinned_ranges[kPinnedRanges];
-    unsigned pinned_next = 0;
+    unsigned pinned_used = 0;
+    uint64_t pinned_epoch = 0;           // g_host_free_epoch when the cache was last valid
+    uint64_t pinned_hits = 0, pinned_misses = 0;  // MSW_HOST_TRACE
     // compat buffers
     uint8_t *c_s1 = nullptr, *c_s2 = nullptr;
     int32_t* c_res = nullptr;
@@ -340,6 +397,7 @@ struct msw_genome {
 namespace msw_detail {
 int ctx_device(const msw_ctx* c) { return c->device; }
 hipStream_t ctx_compute_stream(const msw_ctx* c) { return c->compute; }
+uint64_t ctx_gz_group_bytes(const msw_ctx* c) { return c->opt.gz_group_bytes; }
 }  // namespace msw_detail
 
 namespace {
@@ -348,6 +406,13 @@ int set_device(msw_ctx* ctx) {
     int cur = -1;
     if (hipGetDevice(&cur) == hipSuccess && cur == ctx->device) return MSW_OK;
     HIP_TRY(hipSetDevice(ctx->device));
+    return MSW_OK;
+}
+
+// The streams a context creates on first use (compute is made with it).
+int aux_streams(msw_ctx* ctx) {
+    for (hipStream_t* st : {&ctx->compute2, &ctx->copy, &ctx->d2h, &ctx->side})
+        if (!*st) HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
     return MSW_OK;
 }
 
@@ -475,18 +540,6 @@ int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
     return MSW_OK;
 }
 
-uint64_t default_chunk() {
-    // aligner.rs:9-15 reads GPU_CHUNK_SIZE_READS (mandatory there); here it is
-    // optional and defaults to a size that fills the GPU.
-    const char* v = getenv("GPU_CHUNK_SIZE_READS");
-    if (v && *v) {
-        char* end = nullptr;
-        unsigned long long n = strtoull(v, &end, 10);
-        if (end && *end == '\0' && n > 0) return n;
-    }
-    return 65536;
-}
-
 // Lane-group layout of one launch.  "pairs" scores 2 pairs per G-lane group,
 // "split" 1 pair per group (rows split over the two halves; half the work per
 // wave), "mixed" (G = 16) runs up to one pairs-wave per SIMD and the rest as
@@ -551,11 +604,9 @@ LaunchPlan choose_layout(uint64_t n_pairs, uint32_t max_m, uint32_t max_n, const
         return t;
     };
     const uint32_t stride = msw::stream_stride(max_n);
-    const char* env_g = getenv("MSW_GROUP_LANES");
-    const uint32_t force_g = env_g ? (uint32_t)atoi(env_g) : 0u;
-    const char* env = getenv("MSW_LAYOUT");
-    const bool force_pairs = env && !strcmp(env, "pairs"), force_split = env && !strcmp(env, "split");
-    const bool force_mixed = env && !strcmp(env, "mixed");
+    const uint32_t force_g = sch.opt->group_lanes;
+    const bool force_pairs = sch.opt->force_pairs, force_split = sch.opt->force_split;
+    const bool force_mixed = sch.opt->force_mixed;
 
     LaunchPlan best{msw::Layout::kPairs, 0, 16, 4};
     double best_t = 1e300;
@@ -633,13 +684,13 @@ struct Bucket {
 };
 
 // lengths: the chunk's {min read, max read, min window, max window}.
+// all_long: Options::force_long.
 void bucket_chunk(const uint16_t* rlen, const uint16_t* wlen, uint64_t n, uint32_t* order,
-                  std::vector<Bucket>& buckets, uint32_t lengths[4]) {
+                  std::vector<Bucket>& buckets, uint32_t lengths[4], bool all_long) {
     buckets.clear();
     // key = KR (1..24) * 257 + ceil(n / 16) (<= 256): counting sort; pairs
     // beyond the packed kernels' limits share the last key.
     constexpr int kLongKey = (msw::kMaxRowsPerLane + 1) * 257, kKeys = kLongKey + 1;
-    const bool all_long = force_long();
     auto key_of = [&](uint64_t i) {
         if (all_long || is_long(rlen[i], wlen[i])) return kLongKey;
         const int kr = msw::rows_per_lane(rlen[i], false);
@@ -740,8 +791,8 @@ void fill_multi(const std::vector<Bucket>& buckets, size_t lo, size_t hi, const 
 // Several buckets run as one sw_multi_kernel launch, unless MSW_NO_MULTI is
 // set or a layout / group width is forced (MSW_LAYOUT, MSW_GROUP_LANES): then
 // each bucket gets its own launch with that layout (tests cover both).
-bool use_multi(size_t n_buckets) {
-    return n_buckets > 1 && !getenv("MSW_NO_MULTI") && !getenv("MSW_LAYOUT") && !getenv("MSW_GROUP_LANES");
+bool use_multi(size_t n_buckets, const Options& o) {
+    return n_buckets > 1 && !o.no_multi && !o.layout_set && !o.group_set;
 }
 
 // A long-pair launch next to packed launches runs on the context's side
@@ -759,6 +810,10 @@ struct SideFork {
 };
 
 int fork_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
+    if (!ctx->side) {
+        const int rc = aux_streams(ctx);
+        if (rc) return rc;
+    }
     HIP_TRY(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(f.ev, st));
     HIP_TRY(hipStreamWaitEvent(ctx->side, f.ev, 0));
@@ -773,7 +828,7 @@ int join_side(msw_ctx* ctx, hipStream_t st, SideFork& f) {
 
 // The KR 17..24 buckets as one launch (one launch per bucket measured slower:
 // 8.5 vs 12.7 TCUPS linear).
-bool use_wide_multi(size_t n_wide) { return use_multi(n_wide); }
+bool use_wide_multi(size_t n_wide, const Options& o) { return use_multi(n_wide, o); }
 
 // Where a launch's windows come from: the slot's cut slab (win_stride), or,
 // with a genome, straight from the resident genome at the slot's positions
@@ -824,7 +879,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
     if (g && (use_order || buckets.size() != 1)) return fail(MSW_E_INVALID, "internal: genome windows need one bucket");
     const size_t n_multi = multi_buckets(buckets);
     size_t first_single = 0;
-    if (use_order && use_multi(n_multi)) {
+    if (use_order && use_multi(n_multi, *sch.opt)) {
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
         p.wins = s.d_wins;
@@ -848,7 +903,7 @@ int launch_buckets(msw_ctx* ctx, const Scheme& sch, Slot& s, uint64_t n, const s
     // the KR 17..24 buckets: one launch of the wide instance when there are
     // several (one launch each left each bucket's few waves running alone)
     size_t single_end = n_short;
-    if (use_order && use_wide_multi(n_short - n_multi)) {
+    if (use_order && use_wide_multi(n_short - n_multi, *sch.opt)) {
         msw::SwParams p = base_params(sch);
         p.reads = s.d_reads;
         p.wins = s.d_wins;
@@ -967,7 +1022,7 @@ struct HostBatch {
 // True when [p, p + bytes) lies in page-locked host memory (hipHostMalloc /
 // hipHostRegister): such arrays are DMA'd directly, without staging.
 bool is_pinned(const void* p, size_t bytes) {
-    if (!p || !bytes || getenv("MSW_NO_DIRECT")) return false;
+    if (!p || !bytes) return false;
     for (const void* q : {p, (const void*)((const uint8_t*)p + bytes - 1)}) {
         hipPointerAttribute_t a;
         memset(&a, 0, sizeof(a));
@@ -999,9 +1054,11 @@ void repack_rows(uint8_t* dst, uint32_t dst_stride, const uint8_t* src, uint32_t
     for (uint64_t i = 0; i < n; ++i) memcpy(dst + i * dst_stride, src + i * src_stride, dst_stride);
 }
 
-// MSW_HOST_TRACE=1: per-call host phase times on stderr (tools / DESIGN.md 5).
+// MSW_HOST_TRACE=1 (Options::host_trace): per-call host phase times on
+// stderr (tools / DESIGN.md 5).
 struct HostTrace {
-    bool on = getenv("MSW_HOST_TRACE") != nullptr;
+    bool on;
+    explicit HostTrace(bool enabled) : on(enabled) {}
     double scan = 0, stage = 0, submit = 0, wait = 0;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
     double lap() {
@@ -1075,29 +1132,54 @@ ChunkScan stage_meta(Slot& s, const HostBatch& b, uint64_t first, uint64_t cnt) 
 // True when every pair of the chunk has one bucket key (bucket_chunk's: rows
 // per lane of its read, 16-column blocks of its window, not long) -- decided
 // from the bounds alone, both keys being monotone in the lengths.
-bool single_key(const ChunkScan& c) {
-    return !force_long() && !is_long(c.gm, c.gn) &&
+bool single_key(const ChunkScan& c, bool all_long) {
+    return !all_long && !is_long(c.gm, c.gn) &&
            msw::rows_per_lane(c.lm, false) == msw::rows_per_lane(c.gm, false) &&
            (c.ln + 15) / 16 == (c.gn + 15) / 16;
 }
 
-// Pinned-ness of the caller's arrays, remembered for the last few ranges
-// (hipPointerGetAttributes twice per array and call is a visible share of a
-// small call).  A stale verdict only changes how a copy is made, never what
-// it copies: hipMemcpyAsync accepts pageable and pinned sources alike.
+// Pinned-ness of the caller's arrays, remembered for the most recently used
+// ranges (hipPointerGetAttributes twice per array and call is a visible share
+// of a small call).  msw_host_free bumps g_host_free_epoch, which empties
+// every context's cache at its next lookup, so a freed msw_host_alloc block
+// whose address comes back as pageable memory is never taken for pinned
+// (ADVICE r05).  Memory the caller pins or unpins itself must stay as it was
+// while a call uses it, as for any DMA API; a stale verdict then only changes
+// how a copy is made, never what it copies (hipMemcpyAsync accepts pageable
+// and pinned sources alike, and the d2h copy kernel needs a device pointer
+// for the block, which an unpinned one no longer has).
+std::atomic<uint64_t> g_host_free_epoch{0};
+
 bool pinned_cached(msw_ctx* ctx, const void* p, size_t bytes) {
-    for (const msw_ctx::PinnedRange& r : ctx->pinned_ranges)
-        if (r.p == p && r.bytes == bytes && p) return r.pinned;
+    const uint64_t ep = g_host_free_epoch.load(std::memory_order_acquire);
+    if (ep != ctx->pinned_epoch) {
+        ctx->pinned_used = 0;
+        ctx->pinned_epoch = ep;
+    }
+    msw_ctx::PinnedRange* r = ctx->pinned_ranges;
+    for (unsigned k = 0; k < ctx->pinned_used; ++k)
+        if (r[k].p == p && r[k].bytes == bytes && p) {
+            const msw_ctx::PinnedRange hit = r[k];
+            for (unsigned q = k; q > 0; --q) r[q] = r[q - 1];  // move to front
+            r[0] = hit;
+            ++ctx->pinned_hits;
+            return hit.pinned;
+        }
+    ++ctx->pinned_misses;
     const bool pinned = is_pinned(p, bytes);
-    ctx->pinned_ranges[ctx->pinned_next++ % msw_ctx::kPinnedRanges] = {p, bytes, pinned};
+    const unsigned n = std::min(ctx->pinned_used + 1, msw_ctx::kPinnedRanges);  // the least recent falls off
+    for (unsigned q = n - 1; q > 0; --q) r[q] = r[q - 1];
+    r[0] = {p, bytes, pinned};
+    ctx->pinned_used = n;
     return pinned;
 }
+
 
 int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out_t* out,
                    uint64_t chunk_pairs, bool sync) {
     Scheme sch;
     int rc;
-    if ((rc = make_scheme(sc, &sch))) return rc;
+    if ((rc = make_scheme(sc, ctx->opt, &sch))) return rc;
     if (!out) return fail(MSW_E_INVALID, "out is NULL");
     const bool gmode = b.genome != nullptr;
     const uint64_t n = b.n;
@@ -1109,7 +1191,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     if (n > 0xFFFFFFFFull) return fail(MSW_E_RANGE, "n_pairs > 2^32-1");
     if (gmode && (b.genome->ctx != ctx)) return fail(MSW_E_INVALID, "genome belongs to another context");
     if ((rc = set_device(ctx))) return rc;
-    HostTrace tr;
+    HostTrace tr(ctx->opt.host_trace);
     // Host-side range checks over the whole batch first: fail before any launch.
     // (genome mode bounds the requested window lengths: a clipped window is
     // never longer, and the positions need not be read here)
@@ -1130,7 +1212,7 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
                               : (d_wins ? b.win_stride : std::min(b.win_stride, std::max(16u, round16(gn))));
     if (tr.on) tr.scan += tr.lap();
 
-    const uint64_t chunk = chunk_pairs ? chunk_pairs : default_chunk();
+    const uint64_t chunk = chunk_pairs ? chunk_pairs : ctx->opt.chunk;
     // A multi-chunk call pipelines its own chunks: copies on the copy stream,
     // kernels alternating between the two compute streams, results back on
     // the d2h stream.  A one-chunk call keeps its kernels and results on one
@@ -1140,13 +1222,16 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     // event after the kernels but the timing one).
     const bool multi_chunk = n > chunk;
     const bool alternate = multi_chunk || !sync;
-    const bool direct_out = !multi_chunk && !getenv("MSW_NO_DIRECT_OUT");
+    const bool direct_out = !multi_chunk;
+    // the copy / second compute / d2h streams: created by the first call that uses them
+    if (alternate && !ctx->copy && (rc = aux_streams(ctx))) return rc;
     // Genome mode: a chunk of one bucket that the model puts in the pairs
     // layout with <= 16 rows per lane reads its windows straight from the
     // resident genome (GEN kernel instances: no cut launch, one dependent
-    // step fewer per chunk); other chunks cut a window slab first
-    // (MSW_GENOME_CUT=1 forces the cut for every chunk; tests run both).
-    const bool genome_ok = gmode && !force_long() && !getenv("MSW_GENOME_CUT");
+    // step fewer per chunk); other chunks (several buckets, long pairs, other
+    // layouts) cut a window slab first.
+    const bool all_long = ctx->opt.force_long;
+    const bool genome_ok = gmode && !all_long;
     uint64_t fused_chunks = 0;
     std::vector<Bucket> buckets;
     uint64_t c = 0;
@@ -1159,9 +1244,8 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     // profiles/r05/h2h/chunk_ramp.jsonl): 131k / 262k / 524k chunks 8.29 /
     // 8.49 / 9.41-9.49 ms -> 7.99 / 7.97-8.02 / 8.26-8.56; at 32k the ramp's
     // extra chunk cost 1 % (7.92 -> 8.01), so smaller chunks keep the old
-    // schedule.  MSW_CHUNK_RAMP=0: no ramp.
-    const char* e_ramp = getenv("MSW_CHUNK_RAMP");
-    const bool ramp = chunk > 65536 && !(e_ramp && e_ramp[0] == '0');
+    // schedule.
+    const bool ramp = chunk > 65536;
     uint64_t next_chunk = n > chunk ? std::max<uint64_t>(std::min<uint64_t>(chunk, 8192), chunk / 8) : chunk;
     for (uint64_t first = 0, cnt = 0; first < n; first += cnt, ++c) {
         const uint64_t this_chunk = next_chunk;
@@ -1194,12 +1278,12 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         // positions; the slot order only for a chunk of several buckets.
         const ChunkScan cs_ = stage_meta(s, b, first, cnt);
         bool uniform;
-        if (single_key(cs_)) {  // fixed-length reads and windows, the common case: no sort
+        if (single_key(cs_, all_long)) {  // fixed-length reads and windows, the common case: no sort
             buckets.assign(1, Bucket{0, (uint32_t)cnt, cs_.gm, cs_.gn});
             uniform = true;
         } else {
             uint32_t lens[4];
-            bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets, lens);
+            bucket_chunk(s.h_rlen, s.h_wlen, cnt, s.h_order, buckets, lens, all_long);
             // One read-length bucket: order only matters if windows vary a lot;
             // long pairs of spread read lengths keep their heaviest-first order.
             uniform = buckets.size() == 1 && lens[3] - lens[2] < 16 &&
@@ -1216,11 +1300,10 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         // 54-148 us per 10k-pair batch depending on the box (105-148 on two
         // of three: how the process's streams land on its hardware queues),
         // with the separate upload 55-57 us on every box
-        // (profiles/r05/host/stream_ab*.jsonl).  MSW_ASYNC_ONE_STREAM=1:
-        // the one-stream form.  A synchronous one-chunk call keeps it (no
-        // other call in flight to overlap with).
-        const char* e_one = getenv("MSW_ASYNC_ONE_STREAM");
-        const bool sep_up = multi_chunk || (!sync && !(e_one && e_one[0] == '1'));
+        // (profiles/r05/host/stream_ab*.jsonl).  A synchronous one-chunk
+        // call keeps the one-stream form (no other call in flight to overlap
+        // with).
+        const bool sep_up = multi_chunk || !sync;
         hipStream_t up = sep_up ? ctx->copy : cs;
         HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
         if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
@@ -1283,12 +1366,14 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
     if (tr.on)
         fprintf(stderr,
                 "[msw host] pairs=%llu chunks=%llu direct(reads=%d wins=%d out=%d) genome_chunks=%llu rs=%u ws=%u "
-                "last_launch(layout=%s G=%u KR=%u) scan=%.1fus stage=%.1fus submit=%.1fus wait=%.1fus\n",
+                "last_launch(layout=%s G=%u KR=%u) scan=%.1fus stage=%.1fus submit=%.1fus wait=%.1fus "
+                "pinned_cache(hits=%llu misses=%llu)\n",
                 (unsigned long long)n, (unsigned long long)c, (int)d_reads, (int)d_wins, (int)direct_out,
                 (unsigned long long)fused_chunks, rs, ws,
                 ctx->last_layout == msw::Layout::kSplit ? "split" : (ctx->last_layout == msw::Layout::kMixed ? "mixed" : "pairs"),
                 ctx->last_group_lanes, ctx->last_kr,
-                tr.scan, tr.stage, tr.submit, tr.wait);
+                tr.scan, tr.stage, tr.submit, tr.wait, (unsigned long long)ctx->pinned_hits,
+                (unsigned long long)ctx->pinned_misses);
     return MSW_OK;
 }
 
@@ -1308,11 +1393,8 @@ int run_batch(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, msw_out
     for (Slot& s : ctx->slots) dropped = dropped || (s.busy && s.ticket == ticket);
     if (dropped) {
         const std::string msg = g_last_error;
-        (void)hipStreamSynchronize(ctx->copy);
-        (void)hipStreamSynchronize(ctx->compute);
-        (void)hipStreamSynchronize(ctx->compute2);
-        (void)hipStreamSynchronize(ctx->d2h);
-        (void)hipStreamSynchronize(ctx->side);
+        for (hipStream_t st : {ctx->copy, ctx->compute, ctx->compute2, ctx->d2h, ctx->side})
+            if (st) (void)hipStreamSynchronize(st);
         for (Slot& s : ctx->slots)
             if (s.busy && s.ticket == ticket) s.busy = false;
         ctx->next_ticket++;
@@ -1399,15 +1481,12 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
     if (ordinal < 0 || ordinal >= n) return fail(MSW_E_INVALID, "device %d out of range [0,%d)", ordinal, n);
     msw_ctx* c = new msw_ctx();
     c->device = ordinal;
+    c->opt = read_options();
     hipError_t e = hipSetDevice(ordinal);
     hipDeviceProp_t prop;
     if (e == hipSuccess && hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->epoch);
     if (e == hipSuccess) e = hipEventRecord(c->epoch, c->compute);
     if (e != hipSuccess) {
@@ -1524,8 +1603,7 @@ static int launch_packed(msw_ctx* ctx, const Scheme& sch, msw::SwParams& p, uint
     p.pairs_blocks = plan.pairs_blocks;
     p.group_lanes = plan.group_lanes;
     p.groups = plan.groups;
-    const char* trace_path = getenv("MSW_WAVE_TRACE");
-    if (trace_path && *trace_path) return traced_launch(p, sch, max_read_len, plan, st, trace_path);
+    if (!ctx->opt.wave_trace.empty()) return traced_launch(p, sch, max_read_len, plan, st, ctx->opt.wave_trace.c_str());
     HIP_TRY(msw::launch_sw(p, sch.affine, sch.coords, max_read_len, plan.layout, st));
     return MSW_OK;
 }
@@ -1535,7 +1613,7 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
     Scheme sch;
     int rc;
-    if ((rc = make_scheme(sc, &sch))) return rc;
+    if ((rc = make_scheme(sc, ctx->opt, &sch))) return rc;
     if ((rc = validate_batch(b, out, sch))) return rc;
     if (b->n_pairs == 0) return MSW_OK;
     if ((rc = check_bounds(sch, max_read_len, max_win_len))) return rc;
@@ -1556,7 +1634,7 @@ int msw_align_batch_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_batc
     p.n_slots = (uint32_t)b->n_pairs;
     hipStream_t st = stream ? (hipStream_t)stream : ctx->compute;
     // bounds past the packed kernels: the whole batch on the long-pair kernel
-    if (force_long() || is_long(max_read_len, max_win_len))
+    if (ctx->opt.force_long || is_long(max_read_len, max_win_len))
         return launch_long(sch, p, b->n_pairs, max_read_len, max_win_len, false, ctx->cu_count, st);
     p.win_vec = msw::vec_ok(p.wins, p.win_stride);
     return launch_packed(ctx, sch, p, max_read_len, max_win_len, st);
@@ -1598,7 +1676,7 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
     *out = nullptr;
     Scheme sch;
     int rc;
-    if ((rc = make_scheme(sc, &sch))) return rc;
+    if ((rc = make_scheme(sc, ctx->opt, &sch))) return rc;
     if (n_pairs && (!read_len || !win_len)) return fail(MSW_E_INVALID, "NULL length array");
     if (n_pairs > 0xFFFFFFFFull) return fail(MSW_E_RANGE, "n_pairs > 2^32-1");
     uint32_t gm = 0, gn = 0;
@@ -1619,16 +1697,16 @@ int msw_plan_create(msw_ctx* ctx, const msw_scoring_t* sc, const uint16_t* read_
         std::vector<uint32_t> order(n_pairs);
         std::vector<Bucket> buckets;
         uint32_t lens[4];
-        bucket_chunk(read_len, win_len, n_pairs, order.data(), buckets, lens);
+        bucket_chunk(read_len, win_len, n_pairs, order.data(), buckets, lens, ctx->opt.force_long);
         const size_t n_short = short_buckets(buckets);
         if (n_short < buckets.size()) {
             pl->has_long = true;
             pl->longs = buckets.back();
         }
         const size_t n_multi = multi_buckets(buckets);
-        pl->multi = use_multi(n_multi);
+        pl->multi = use_multi(n_multi, ctx->opt);
         if (pl->multi) fill_multi(buckets, 0, n_multi, sch, pl->table);
-        pl->wide = use_wide_multi(n_short - n_multi);
+        pl->wide = use_wide_multi(n_short - n_multi, ctx->opt);
         if (pl->wide) fill_multi(buckets, n_multi, n_short, sch, pl->wide_table);
         for (size_t bi = pl->multi ? n_multi : 0; bi < (pl->wide ? n_multi : n_short); ++bi)
             pl->singles.push_back({buckets[bi], choose_layout(buckets[bi].count, buckets[bi].max_m, buckets[bi].max_n,
@@ -1812,9 +1890,11 @@ int msw_genome_create(msw_ctx* ctx, const uint8_t* seq, uint64_t len, msw_genome
         delete g;
         return fail(MSW_E_NOMEM, "hipMalloc(%llu B) for the genome: %s", (unsigned long long)len, hipGetErrorString(e));
     }
-    e = hipMemsetAsync(g->d_seq + len, 0, msw::kGenomePad, ctx->copy);
-    if (e == hipSuccess && len) e = hipMemcpyAsync(g->d_seq, seq, len, hipMemcpyHostToDevice, ctx->copy);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->copy);
+    // on the compute stream (the call is synchronous; a --full-wgs worker
+    // then never creates its copy stream)
+    e = hipMemsetAsync(g->d_seq + len, 0, msw::kGenomePad, ctx->compute);
+    if (e == hipSuccess && len) e = hipMemcpyAsync(g->d_seq, seq, len, hipMemcpyHostToDevice, ctx->compute);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->compute);
     if (e != hipSuccess) {
         msw_genome_destroy(g);
         return fail(MSW_E_DEVICE, "genome upload: %s", hipGetErrorString(e));
@@ -1915,8 +1995,10 @@ int msw_memcpy_d2h_async(msw_ctx* ctx, void* dst, const void* src, size_t bytes,
     // shared in-order rings, so a DMA that waits on its stream's scoring
     // kernel holds up the copies other workers queued behind it (config 3
     // from FASTQ: one worker's result copies 2 ms late, behind the other's
-    // next batch).  MSW_D2H_DMA=1 keeps the DMA.
-    if (bytes && !getenv("MSW_D2H_DMA") && pinned_cached(ctx, dst, bytes)) {
+    // next batch).  Source and destination that differ in
+    // alignment mod 16 go by DMA: the kernel would copy them byte by byte
+    // (ADVICE r05).
+    if (bytes && (((uintptr_t)dst ^ (uintptr_t)src) & 15) == 0 && pinned_cached(ctx, dst, bytes)) {
         void* dp = nullptr;
         if (hipHostGetDevicePointer(&dp, dst, 0) == hipSuccess && dp) {
             HIP_TRY(msw::launch_d2h_copy(dp, src, bytes, st));
@@ -1939,7 +2021,9 @@ void* msw_host_alloc(size_t bytes) {
 }
 
 void msw_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    (void)hipHostFree(p);
+    g_host_free_epoch.fetch_add(1, std::memory_order_release);  // every context's pinned cache is stale
 }
 
 void* msw_dev_alloc(msw_ctx* ctx, size_t bytes) {
@@ -1977,7 +2061,7 @@ int msw_ctx_prepare(msw_ctx* ctx, const msw_scoring_t* sc) {
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
     Scheme sch;
     int rc;
-    if ((rc = make_scheme(sc, &sch))) return rc;
+    if ((rc = make_scheme(sc, ctx->opt, &sch))) return rc;
     if ((rc = set_device(ctx))) return rc;
     // one occupancy query per kernel module (translation unit): the query
     // loads the module; the shapes are any valid ones of that unit
@@ -2056,10 +2140,8 @@ int msw_synchronize(msw_ctx* ctx) {
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
     int rc = set_device(ctx);
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(ctx->compute));
-    HIP_TRY(hipStreamSynchronize(ctx->compute2));
-    HIP_TRY(hipStreamSynchronize(ctx->copy));
-    HIP_TRY(hipStreamSynchronize(ctx->d2h));
+    for (hipStream_t st : {ctx->compute, ctx->compute2, ctx->copy, ctx->d2h, ctx->side})
+        if (st) HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipGetLastError());
     return MSW_OK;
 }

@@ -33,3 +33,34 @@ def gpu_ctx():
     ctx = Context(0)
     yield ctx
     ctx.close()
+
+
+class FreshCtx:
+    """A Context made at its first use, under the environment of that moment:
+    the library reads its switches (MSW_LAYOUT, MSW_NO_F16, MSW_HOST_TRACE,
+    ...) once, when a context is created, so a test that sets one uses a
+    context of its own (closed at teardown)."""
+
+    def __init__(self):
+        self._c = None
+
+    def __getattr__(self, k):
+        if k.startswith("__"):
+            raise AttributeError(k)
+        if self._c is None:
+            from mini_parallel_amd import Context
+            self._c = Context(0)
+        return getattr(self._c, k)
+
+    def close(self):
+        if self._c is not None:
+            self._c.close()
+            self._c = None
+
+
+@pytest.fixture
+def fresh_ctx():
+    import torch  # noqa: F401  (as gpu_ctx: libmsw.so binds torch's HIP runtime)
+    c = FreshCtx()
+    yield c
+    c.close()

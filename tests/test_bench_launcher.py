@@ -111,11 +111,13 @@ def _check_extras(d, world):
     p = c4["parity"]
     assert p["files_once"] and p["files_done"] == 16 and p["reads"] == p["reads_expected"] == 16 * 120
     assert p["file0_ok"] is True and p["rows_ok"] is True and p["files_checked"] == 16
+    assert p["files_by_rank"] == [list(range(r, 16, world)) for r in range(world)] and p["files_sharded_as_cli"]
     assert c4["reads_per_s"] > 0 and c4["gcups"] > 0
     assert c4["segments"] == {**c4["segments"], "pool": 5, "segment_reads": 40, "segments_per_file": 3}
     f3 = ex["config3"]["fastq"]  # per-read records of 2N lane files, gathered in file order
     assert f3["n_ranks"] == world and f3["reads"] == 320 * world and f3["scaling"] == "weak"
     assert f3["parity"]["bit_exact"] is True and f3["parity"]["records_checked"] == 320 * world
+    assert f3["parity"]["files_by_rank"] == [[r, r + world] for r in range(world)]
     # one rank's two lane files generated and scored, byte-identical copies for the rest
     ds = f3["dataset"]
     assert ds["files_generated"] == 2 and ds["files_copied"] == 2 * world - 2, ds

@@ -43,24 +43,6 @@ def host_windows(genome: np.ndarray, pos: np.ndarray, want: np.ndarray):
     return W, eff.astype(np.uint16)
 
 
-@pytest.fixture(autouse=True, params=["genome_windows", "cut_slab", "copy_back"])
-def window_source(request, monkeypatch):
-    """Every test of this module three times: the packed kernels reading each
-    window straight from the resident genome (the default), the windows first
-    cut into a slab (MSW_GENOME_CUT=1, also the path of long pairs), and that
-    with one-chunk calls copying their results back instead of the kernels
-    storing them into the slot's mapped host block (MSW_NO_DIRECT_OUT=1)."""
-    if request.param == "genome_windows":
-        monkeypatch.delenv("MSW_GENOME_CUT", raising=False)
-    else:
-        monkeypatch.setenv("MSW_GENOME_CUT", "1")
-    if request.param == "copy_back":
-        monkeypatch.setenv("MSW_NO_DIRECT_OUT", "1")
-    else:
-        monkeypatch.delenv("MSW_NO_DIRECT_OUT", raising=False)
-    return request.param
-
-
 def assert_same(got, want, coords):
     s, i, j = got
     ws, wi, wj = want
@@ -163,12 +145,13 @@ def test_genome_with_other_bytes(gpu_ctx, oracle):
 
 @pytest.mark.parametrize("sc", SCHEMES, ids=["linear", "linear_coords", "affine_coords"])
 @pytest.mark.parametrize("n,chunk", [(10_000, 0), (9_000, 2_500), (37, 0)])
-def test_genome_uniform_chunks(gpu_ctx, oracle, sc, n, chunk, monkeypatch, capfd, window_source):
+def test_genome_uniform_chunks(fresh_ctx, oracle, sc, n, chunk, monkeypatch, capfd):
     """Chunks of one length bucket (150 bp reads, 289..300-byte windows: the
     config-2 shape from the genome) -- the chunks the scoring kernels score
     with windows read straight from the genome: every window start residue
     mod 16, windows clipped a few bytes short at the genome end, reads with
-    N; async calls as bench.py streams them.  MSW_HOST_TRACE shows the path."""
+    N; async calls as bench.py streams them.  MSW_HOST_TRACE shows the path
+    (the library reads it when the context is made: fresh_ctx)."""
     rng = np.random.default_rng(n + chunk)
     g = rng.choice(ACGT, 3_000_017)
     pos = rng.integers(0, g.size - 300, n).astype(np.int64)
@@ -180,22 +163,22 @@ def test_genome_uniform_chunks(gpu_ctx, oracle, sc, n, chunk, monkeypatch, capfd
     for k in range(n):
         R[k, :150] = g[pos[k] + 70:pos[k] + 220] if pos[k] + 220 <= g.size else rng.choice(ACGT, 150)
     R[5, 40:44] = ord("N")
-    genome = gpu_ctx.load_genome(g)
+    genome = fresh_ctx.load_genome(g)
     W, wl = host_windows(g, pos, want)
     expect = oracle_run(oracle, R, rl, W, wl, sc)
     monkeypatch.setenv("MSW_HOST_TRACE", "1")
     capfd.readouterr()
-    assert_same(gpu_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk), expect, sc.want_coords)
+    assert_same(fresh_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk), expect, sc.want_coords)
     trace = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")]
     chunks = int(trace[-1].split("chunks=")[1].split()[0])
     genome_chunks = int(trace[-1].split("genome_chunks=")[1].split()[0])
     direct_out = int(trace[-1].split("direct(")[1].split("out=")[1].split(")")[0])
-    assert direct_out == (0 if window_source == "copy_back" or chunks > 1 else 1), trace[-1]
-    if window_source != "genome_windows":
-        assert genome_chunks == 0, trace[-1]
-    elif n == 10_000:  # the config-2 shape: one chunk, pairs layout (smaller chunks may take the split layout)
+    # one-chunk calls: the kernels store into the slot's mapped block; more
+    # chunks copy their results back
+    assert direct_out == (0 if chunks > 1 else 1), trace[-1]
+    if n == 10_000:  # the config-2 shape: one chunk, pairs layout (smaller chunks may take the split layout)
         assert genome_chunks == chunks == 1, trace[-1]
-    pend = [gpu_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk, asynchronous=True)
+    pend = [fresh_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk, asynchronous=True)
             for _ in range(3)]
     for p in pend[::-1]:
         assert_same(p.wait(), expect, sc.want_coords)
@@ -237,14 +220,21 @@ def test_align_reads_device(gpu_ctx, oracle, window):
     genome.close()
 
 
-def test_genome_mixed_lengths_bucketed(gpu_ctx, oracle):
-    """Config 5 shape through the genome path (length-bucketed launch)."""
+def test_genome_mixed_lengths_bucketed(fresh_ctx, oracle, monkeypatch, capfd):
+    """Config 5 shape through the genome path (length-bucketed launch): a
+    chunk of several buckets cuts its windows into a slab first (no chunk
+    reads the genome directly; MSW_HOST_TRACE shows it), and equals the
+    oracle."""
     g, R, rl, pos, want = genome_case(8000, 2_000_000, seed=21, read_stride=256)
     rl[:] = np.random.default_rng(3).integers(75, 251, rl.size)
     want[:] = 2 * rl
-    genome = gpu_ctx.load_genome(g)
+    monkeypatch.setenv("MSW_HOST_TRACE", "1")
+    genome = fresh_ctx.load_genome(g)
     for sc in SCHEMES[1:]:
-        got = gpu_ctx.align_reads(genome, R, rl, pos, want, sc)
+        capfd.readouterr()
+        got = fresh_ctx.align_reads(genome, R, rl, pos, want, sc)
+        line = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")][-1]
+        assert int(line.split("genome_chunks=")[1].split()[0]) == 0, line
         W, wl = host_windows(g, pos, want)
         assert_same(got, oracle_run(oracle, R, rl, W, wl, sc), True)
 
@@ -266,9 +256,10 @@ def test_genome_errors(gpu_ctx):
 
 
 @pytest.mark.parametrize("sc", SCHEMES[1:], ids=["linear_coords", "affine_coords"])
-def test_pinned_direct_and_staged_agree(gpu_ctx, oracle, monkeypatch, sc):
-    """Pinned arrays are DMA'd from the caller's memory; pageable ones are
-    staged; MSW_NO_DIRECT forces staging of pinned arrays.  All bit-exact."""
+def test_pinned_direct_and_staged_agree(fresh_ctx, oracle, monkeypatch, capfd, sc):
+    """Pinned arrays are DMA'd from the caller's memory, pageable ones are
+    staged (MSW_HOST_TRACE shows which); one chunk and several.  All
+    bit-exact."""
     b = make_pairs(9000, 150, 2.0, seed=77, read_stride=160, win_stride=304)
     want = oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc)
     pr = pinned_empty(b.reads.shape, np.uint8)
@@ -276,15 +267,13 @@ def test_pinned_direct_and_staged_agree(gpu_ctx, oracle, monkeypatch, sc):
     prl = pinned_empty(b.read_len.shape, np.uint16)
     pwl = pinned_empty(b.win_len.shape, np.uint16)
     pr[:], pw[:], prl[:], pwl[:] = b.reads, b.wins, b.read_len, b.win_len
-    for direct in (True, False):
-        if direct:
-            monkeypatch.delenv("MSW_NO_DIRECT", raising=False)
-        else:
-            monkeypatch.setenv("MSW_NO_DIRECT", "1")
+    monkeypatch.setenv("MSW_HOST_TRACE", "1")
+    for arrs, direct in (((pr, prl, pw, pwl), 1), ((b.reads, b.read_len, b.wins, b.win_len), 0)):
         for chunk in (0, 2500):
-            assert_same(gpu_ctx.align_batch(pr, prl, pw, pwl, sc, chunk_pairs=chunk), want, True)
-    monkeypatch.delenv("MSW_NO_DIRECT", raising=False)
-    assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc), want, True)
+            capfd.readouterr()
+            assert_same(fresh_ctx.align_batch(*arrs, sc, chunk_pairs=chunk), want, True)
+            line = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")][-1]
+            assert f"direct(reads={direct} wins={direct}" in line, line
 
 
 def test_wide_strides_repacked(gpu_ctx, oracle):
@@ -394,13 +383,11 @@ def test_error_paths(gpu_ctx):
     assert list(p.wait()[0]) == [0, 0]  # zero reads vs ACGT: nothing matches byte 0
 
 
-@pytest.mark.parametrize("one_stream", ["0", "1"])
-def test_async_stream_upload_forms(gpu_ctx, oracle, monkeypatch, one_stream, window_source):
+def test_async_stream_upload_forms(gpu_ctx, oracle):
     """A stream of one-chunk async calls (the host-to-host stream of bench.py,
-    three in flight, results waited oldest first and newest first): uploads
-    on the copy stream behind an event (default) or on the call's compute
-    stream (MSW_ASYNC_ONE_STREAM=1); every batch equals the oracle."""
-    monkeypatch.setenv("MSW_ASYNC_ONE_STREAM", one_stream)
+    three in flight, results waited oldest first and newest first; uploads on
+    the copy stream behind an event) between synchronous one-chunk calls
+    (uploads on the compute stream); every batch equals the oracle."""
     rng = np.random.default_rng(17)
     g = rng.choice(ACGT, 1_000_003)
     n = 3_000
@@ -420,5 +407,11 @@ def test_async_stream_upload_forms(gpu_ctx, oracle, monkeypatch, one_stream, win
         if len(pend) == 3:
             assert_same(pend.pop(0).wait(), expect, sc.want_coords)
     for p in pend[::-1]:
+        assert_same(p.wait(), expect, sc.want_coords)
+    pend = []
+    for k in range(4):  # synchronous and async calls interleaved
+        pend.append(gpu_ctx.align_reads(genome, R, rl, pos, want, sc, asynchronous=True))
+        assert_same(gpu_ctx.align_reads(genome, R, rl, pos, want, sc), expect, sc.want_coords)
+    for p in pend:
         assert_same(p.wait(), expect, sc.want_coords)
     genome.close()

@@ -118,7 +118,7 @@ def test_inflate_large_many_spans(gpu_ctx):
     assert bgzf_inflate(gpu_ctx, blob) == data
 
 
-def test_inflate_long_run_of_empty_members(gpu_ctx, monkeypatch):
+def test_inflate_long_run_of_empty_members(fresh_ctx, monkeypatch):
     """members of ISIZE 0 (BGZF EOF blocks) add compressed bytes
     but no output, so a group bounded only by its output size could copy
     more compressed bytes than the pinned staging holds.  With 1 MiB groups
@@ -131,7 +131,7 @@ def test_inflate_long_run_of_empty_members(gpu_ctx, monkeypatch):
     tail = bgzf_compress(data[len(data) // 2:], 6)
     blob = head + BGZF_EOF * 250_000 + tail
     assert len(blob) > 7_000_000
-    assert bgzf_inflate(gpu_ctx, blob) == data
+    assert bgzf_inflate(fresh_ctx, blob) == data  # MSW_GZ_GROUP_MB: read when the context is made
 
 
 def test_inflate_errors(gpu_ctx):
@@ -306,16 +306,17 @@ def test_reader_prefetch_chain(gpu_ctx, tmp_path, monkeypatch, span):
 
 @pytest.mark.parametrize("threads", ["3", "8"])
 def test_reader_parallel_compressed_reads(gpu_ctx, tmp_path, monkeypatch, threads):
-    """Compressed top-ups split over several positioned-read threads
-    (MSW_GZ_READ_THREADS; MSW_GZ_READ_SPLIT lowers the 32 MiB threshold so a
-    small file takes the split path, with parts ending mid-member)."""
+    """Compressed top-ups of 32 MiB or more split over several positioned-read
+    threads (MSW_GZ_READ_THREADS), parts ending mid-member: a lane file of
+    stored (level 0) BGZF members, ~35 MB, read in copied mode."""
     monkeypatch.setenv("MSW_GZ_NO_MAP", "1")
     monkeypatch.setenv("MSW_GZ_READ_THREADS", threads)
-    monkeypatch.setenv("MSW_GZ_READ_SPLIT", "4099")
-    data = fastq_text(20_000, 23)
+    data = fastq_text(100_000, 23)
+    blob = bgzf_compress(data, 0, block=0xFF00)
+    assert len(blob) >= 32 << 20
     p = tmp_path / "lane.fastq.gz"
-    p.write_bytes(bgzf_compress(data, 6, block=0xFF00))
-    assert assert_reader_parity(gpu_ctx, str(p)) == 20_000
+    p.write_bytes(blob)
+    assert assert_reader_parity(gpu_ctx, str(p)) == 100_000
 
 
 @pytest.mark.parametrize("mode", ["map", "map_upload", "copy"])

@@ -1,11 +1,13 @@
 """Every environment knob the product still reads, exercised on the GPU (the
 other knobs are covered where their paths are tested: MSW_LAYOUT /
 MSW_GROUP_LANES / MSW_NO_MULTI / MSW_NO_F16 in test_gpu_parity.py,
-MSW_FORCE_LONG / MSW_LONG_BLOCKS in test_gpu_long.py, MSW_NO_DIRECT in
+MSW_FORCE_LONG / MSW_LONG_BLOCKS in test_gpu_long.py, MSW_HOST_TRACE in
 test_gpu_genome.py, the MSW_GZ_* reader knobs in test_gpu_gz.py, MSW_DEVICES /
 MSW_GPU_INFLATE / MSW_GFASTQ_BATCH / MSW_GFASTQ_SPAN_MB / MSW_MAX_READ_LEN in
 test_cli.py; INTEGRATION.md lists them all).  Tracing knobs must not change
-results; tuning knobs must not change results either."""
+results; tuning knobs must not change results either.  The library reads
+its knobs once, when a context (or a GPU lane reader) is made: tests that
+set one use a context of their own."""
 import json
 import os
 import re

@@ -135,7 +135,7 @@ def test_wide_buckets_one_launch(gpu_ctx, oracle, kind):
 
 @pytest.mark.parametrize("blocks", ["1", "7", "0"])
 @pytest.mark.parametrize("kind", ["linear", "affine_coords"])
-def test_long_work_queue(gpu_ctx, oracle, monkeypatch, kind, blocks):
+def test_long_work_queue(fresh_ctx, oracle, monkeypatch, kind, blocks):
     """Long pairs of spread lengths (sorted heaviest first by the host) with
     fewer blocks than pairs (MSW_LONG_BLOCKS; "0" = the default grid): the
     blocks take slots from the launch's work queue -- host batches, the device
@@ -145,23 +145,23 @@ def test_long_work_queue(gpu_ctx, oracle, monkeypatch, kind, blocks):
     sc = scoring(kind)
     b = make_pairs(90, (257, 1300), seed=77)
     want = oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc)
-    assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc), want, sc.want_coords)
+    assert_same(fresh_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc), want, sc.want_coords)
     n = b.n_pairs
     dR, dW, drl, dwl = _device([b.reads, b.wins, b.read_len.view(np.int16), b.win_len.view(np.int16)])
     score, ei, ej = _device([np.zeros(n, np.int32), np.zeros(n, np.int16), np.zeros(n, np.int16)])
-    gpu_ctx.align_batch_device(dR.data_ptr(), drl.data_ptr(), dW.data_ptr(), dwl.data_ptr(), b.reads.shape[1],
+    fresh_ctx.align_batch_device(dR.data_ptr(), drl.data_ptr(), dW.data_ptr(), dwl.data_ptr(), b.reads.shape[1],
                                b.wins.shape[1], n, score.data_ptr(), int(b.read_len.max()), int(b.win_len.max()), sc,
                                ei.data_ptr(), ej.data_ptr())
     torch.cuda.synchronize()
-    gpu_ctx.synchronize()
+    fresh_ctx.synchronize()
     assert_same((score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy()), want, sc.want_coords)
     score.zero_()
-    launch = gpu_ctx.prepare_planned_launch(dR.data_ptr(), drl.data_ptr(), dW.data_ptr(), dwl.data_ptr(),
+    launch = fresh_ctx.prepare_planned_launch(dR.data_ptr(), drl.data_ptr(), dW.data_ptr(), dwl.data_ptr(),
                                             b.reads.shape[1], b.wins.shape[1], b.read_len, b.win_len,
                                             score.data_ptr(), sc, ei.data_ptr(), ej.data_ptr())
     try:
         launch()
-        gpu_ctx.synchronize()
+        fresh_ctx.synchronize()
         assert_same((score.cpu().numpy(), ei.cpu().numpy(), ej.cpu().numpy()), want, sc.want_coords)
     finally:
         launch.close()
@@ -300,13 +300,13 @@ def test_long_genome_reads(gpu_ctx, oracle, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-def test_long_kernel_on_short_shapes(gpu_ctx, oracle, monkeypatch, kind):
+def test_long_kernel_on_short_shapes(fresh_ctx, oracle, monkeypatch, kind):
     """MSW_FORCE_LONG=1: the long-pair kernel over the packed kernels' own
     shapes (config-2 pairs, mixed 75-250 bp reads) -- one strip, R = 1..4."""
     monkeypatch.setenv("MSW_FORCE_LONG", "1")
     sc = scoring(kind)
     for b in (make_pairs(3000, 150, seed=31), make_pairs(2000, (1, 250), seed=32)):
-        assert_same(gpu_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc),
+        assert_same(fresh_ctx.align_batch(b.reads, b.read_len, b.wins, b.win_len, sc),
                     oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc), sc.want_coords)
 
 
@@ -330,7 +330,7 @@ def test_long_random_sizes(gpu_ctx, oracle, kind):
 
 @pytest.mark.parametrize("env", [{"MSW_NO_MULTI": "1"}, {"MSW_LAYOUT": "split"}, {"MSW_LAYOUT": "pairs", "MSW_GROUP_LANES": "12"},
                                  {"MSW_NO_F16": "1"}])
-def test_long_beside_forced_layouts(gpu_ctx, oracle, monkeypatch, env):
+def test_long_beside_forced_layouts(fresh_ctx, oracle, monkeypatch, env):
     """The long bucket next to per-bucket launches of the packed kernels
     (forced layouts, no single multi launch) and next to the integer path."""
     for k, v in env.items():
@@ -346,4 +346,4 @@ def test_long_beside_forced_layouts(gpu_ctx, oracle, monkeypatch, env):
         reads.insert(at, r)
         wins.insert(at, w)
     R, rl, W, wl = mpa.pack_batch(reads, wins)
-    assert_same(gpu_ctx.align_batch(R, rl, W, wl, sc, chunk_pairs=300), oracle_run(oracle, R, rl, W, wl, sc), True)
+    assert_same(fresh_ctx.align_batch(R, rl, W, wl, sc, chunk_pairs=300), oracle_run(oracle, R, rl, W, wl, sc), True)

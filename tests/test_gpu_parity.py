@@ -76,42 +76,42 @@ def test_device_visible(gpu_ctx):
     ("linear_2_-1_2", Scoring(want_coords=True)),
     ("affine_2_-1_o3_e1", Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)),
 ])
-def test_kat(gpu_ctx, layout, section, sc):
+def test_kat(fresh_ctx, layout, section, sc):
     kats = json.load(open(os.path.join(GOLDEN, "kat.json")))[section]
     R, rl, W, wl = mpa.pack_batch([k["read"].encode() for k in kats], [k["window"].encode() for k in kats])
-    s, i, j = gpu_ctx.align_batch(R, rl, W, wl, sc)
+    s, i, j = fresh_ctx.align_batch(R, rl, W, wl, sc)
     for k, a, b, c in zip(kats, s, i, j):
         assert (int(a), int(b), int(c)) == (k["score"], k["end_i"], k["end_j"]), k
 
 
 @pytest.mark.parametrize("name", ["linear_150x300.npz", "affine_150x300.npz", "mixed_linear.npz"])
 @pytest.mark.parametrize("coords", [False, True])
-def test_golden(gpu_ctx, layout, name, coords):
+def test_golden(fresh_ctx, layout, name, coords):
     z = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
     meta = json.loads(str(z["meta"]))
     sc = Scoring(match=meta["match"], mismatch=meta["mismatch"], gap_open=meta.get("gap_open", 0),
                  gap_extend=meta["gap_extend"], affine=meta["affine"], want_coords=coords)
-    got = gpu_ctx.align_batch(z["reads"], z["read_len"], z["wins"], z["win_len"], sc)
+    got = fresh_ctx.align_batch(z["reads"], z["read_len"], z["wins"], z["win_len"], sc)
     assert_same(got, (z["score"], z["end_i"], z["end_j"]), coords)
 
 
-def test_config2_linear_score_only(gpu_ctx, layout, oracle):
+def test_config2_linear_score_only(fresh_ctx, layout, oracle):
     """BASELINE config 2 at full size: 10k x (150 bp, 300 bp), linear, score-only."""
     b = config_batch(2)
     sc = Scoring()
-    assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), False)
+    assert_same(gpu_run(fresh_ctx, b, sc), oracle_run(oracle, b, sc), False)
 
 
-def test_config3_affine_coords_sample(gpu_ctx, layout, oracle):
+def test_config3_affine_coords_sample(fresh_ctx, layout, oracle):
     """Config 3 shape (affine + best cell), chunked through the pinned pipeline."""
     b = config_batch(3, n_pairs=40_000)
     sc = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)
-    assert_same(gpu_run(gpu_ctx, b, sc, chunk=9_000), oracle_run(oracle, b, sc), True)
+    assert_same(gpu_run(fresh_ctx, b, sc, chunk=9_000), oracle_run(oracle, b, sc), True)
 
 
 @pytest.mark.parametrize("sc", [Scoring(), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)],
                          ids=["linear", "affine_coords"])
-def test_narrow_groups_large_batch(gpu_ctx, oracle, monkeypatch, capfd, sc):
+def test_narrow_groups_large_batch(fresh_ctx, oracle, monkeypatch, capfd, sc):
     """A batch large enough (>= 48 waves per SIMD of 16-pair waves, sized
     from this GPU's CU count) that the layout model takes narrow lane groups
     of 17..19 rows (150 bp reads: G = 8 or 9) on its own, as one launch --
@@ -123,7 +123,7 @@ def test_narrow_groups_large_batch(gpu_ctx, oracle, monkeypatch, capfd, sc):
     b = config_batch(3, n_pairs=n)
     monkeypatch.setenv("MSW_HOST_TRACE", "1")
     capfd.readouterr()
-    got = gpu_run(gpu_ctx, b, sc, chunk=n)
+    got = gpu_run(fresh_ctx, b, sc, chunk=n)
     line = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")][-1]
     plan = line.split("last_launch(")[1].split(")")[0]
     g = int(plan.split("G=")[1].split()[0])
@@ -145,7 +145,7 @@ def _last_plan(capfd):
 @pytest.mark.parametrize("n", [131_072, 262_144, 524_288])
 @pytest.mark.parametrize("sc", [Scoring(), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)],
                          ids=["linear", "affine_coords"])
-def test_narrow_gate_mid_batches(gpu_ctx, oracle, monkeypatch, capfd, sc, n):
+def test_narrow_gate_mid_batches(fresh_ctx, oracle, monkeypatch, capfd, sc, n):
     """Config-3 batches (150 bp reads) either side of the measured narrow-group
     crossover, each at the layout model's own choice: 9-lane groups of 17 rows
     (14 pairs per wave) are taken from 16 waves per SIMD on (229k pairs on 256
@@ -157,7 +157,7 @@ def test_narrow_gate_mid_batches(gpu_ctx, oracle, monkeypatch, capfd, sc, n):
     b = config_batch(3, n_pairs=n, seed_offset=n % 977)
     monkeypatch.setenv("MSW_HOST_TRACE", "1")
     capfd.readouterr()
-    got = gpu_run(gpu_ctx, b, sc, chunk=n)
+    got = gpu_run(fresh_ctx, b, sc, chunk=n)
     line, lay, g, kr = _last_plan(capfd)
     if kr > 16:  # a narrow launch: only past its family's measured gate
         per = 2 * (64 // g)
@@ -170,22 +170,22 @@ def test_narrow_gate_mid_batches(gpu_ctx, oracle, monkeypatch, capfd, sc, n):
     assert_same(got, (s, i, j), sc.want_coords)
 
 
-def test_config5_mixed_lengths(gpu_ctx, layout, oracle):
+def test_config5_mixed_lengths(fresh_ctx, layout, oracle):
     """Config 5 shape: 75-250 bp reads, window 2m, length-bucketed dispatch."""
     b = config_batch(5, n_pairs=12_000)
     for sc in (Scoring(want_coords=True), Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)):
-        assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
+        assert_same(gpu_run(fresh_ctx, b, sc), oracle_run(oracle, b, sc), True)
 
 
 @pytest.mark.parametrize("coords", [False, True])
 @pytest.mark.parametrize("affine", [False, True])
-def test_integer_domain_on_acgt(gpu_ctx, layout, oracle, monkeypatch, affine, coords):
+def test_integer_domain_on_acgt(fresh_ctx, layout, oracle, monkeypatch, affine, coords):
     """MSW_NO_F16 forces the u16 integer path (xor/min substitution) on
     ACGT windows that would otherwise take the f16 table path."""
     monkeypatch.setenv("MSW_NO_F16", "1")
     b = config_batch(2, n_pairs=3000, seed_offset=91)
     sc = Scoring(gap_open=3 if affine else 0, gap_extend=1 if affine else 2, affine=affine, want_coords=coords)
-    assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), coords)
+    assert_same(gpu_run(fresh_ctx, b, sc), oracle_run(oracle, b, sc), coords)
 
 
 @pytest.mark.parametrize("match,mismatch,go,ge,affine", [
@@ -196,13 +196,13 @@ def test_integer_domain_on_acgt(gpu_ctx, layout, oracle, monkeypatch, affine, co
     # gap penalties of 2048 and more (capped in the f16 domain)
     (2, -1, 0, 1024, False), (2, -1, 5000, 1024, True),
 ])
-def test_scoring_schemes(gpu_ctx, layout, oracle, match, mismatch, go, ge, affine):
+def test_scoring_schemes(fresh_ctx, layout, oracle, match, mismatch, go, ge, affine):
     b = make_pairs(3000, (1, 200), 1.7, seed=match * 100 + ge, read_stride=208, win_stride=352)
     sc = Scoring(match=match, mismatch=mismatch, gap_open=go, gap_extend=ge, affine=affine, want_coords=True)
-    assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
+    assert_same(gpu_run(fresh_ctx, b, sc), oracle_run(oracle, b, sc), True)
 
 
-def test_edge_lengths(gpu_ctx, layout, oracle):
+def test_edge_lengths(fresh_ctx, layout, oracle):
     """Empty, 1-base, 16k+/-1 boundaries, max read 256, long windows, byte zoo."""
     rng = np.random.default_rng(17)
     lens_r = [0, 1, 2, 15, 16, 17, 31, 32, 33, 150, 255, 256, 256, 7, 0, 100]
@@ -218,10 +218,10 @@ def test_edge_lengths(gpu_ctx, layout, oracle):
     R, rl, W, wl = mpa.pack_batch(reads * 3, wins * 3)
     b = B(R, rl, W, wl)
     for sc in (Scoring(want_coords=True), Scoring(gap_open=2, gap_extend=1, affine=True, want_coords=True)):
-        assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), True)
+        assert_same(gpu_run(fresh_ctx, b, sc), oracle_run(oracle, b, sc), True)
 
 
-def test_identical_and_all_mismatch(gpu_ctx, layout, oracle):
+def test_identical_and_all_mismatch(fresh_ctx, layout, oracle):
     rng = np.random.default_rng(23)
     seqs = [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 150)) for _ in range(64)]
     reads = seqs + [b"A" * 150] * 8 + [b"N" * 150] * 8
@@ -229,13 +229,13 @@ def test_identical_and_all_mismatch(gpu_ctx, layout, oracle):
     R, rl, W, wl = mpa.pack_batch(reads, wins)
     b = B(R, rl, W, wl)
     sc = Scoring(want_coords=True)
-    got = gpu_run(gpu_ctx, b, sc)
+    got = gpu_run(fresh_ctx, b, sc)
     assert_same(got, oracle_run(oracle, b, sc), True)
     assert all(got[0][:64] == 300) and all(got[0][64:72] == 0) and all(got[1][64:72] == -1)
     assert all(got[0][72:] == 300)
 
 
-def test_acgt_fast_path_and_fallback(gpu_ctx, layout, oracle):
+def test_acgt_fast_path_and_fallback(fresh_ctx, layout, oracle):
     """Waves whose windows are pure A/C/G/T take the v_perm table path (reads
     may hold any byte: N, lower case, bytes whose class formula collides with
     A/C/G/T such as 'E', high-bit bytes); a window with any other byte sends its
@@ -260,7 +260,7 @@ def test_acgt_fast_path_and_fallback(gpu_ctx, layout, oracle):
     for sc in (Scoring(want_coords=True), Scoring(),
                Scoring(gap_open=2, gap_extend=1, affine=True, want_coords=True),
                Scoring(match=3, mismatch=-61, gap_open=7, gap_extend=1024, affine=True)):
-        assert_same(gpu_run(gpu_ctx, b, sc), oracle_run(oracle, b, sc), sc.want_coords)
+        assert_same(gpu_run(fresh_ctx, b, sc), oracle_run(oracle, b, sc), sc.want_coords)
 
 
 def test_async_and_chunking_agree(gpu_ctx, oracle):
@@ -364,7 +364,7 @@ def test_range_errors(gpu_ctx, bad):
         gpu_ctx.align_batch(R, rl, W, wl, sc)
 
 
-def test_device_resident_api(gpu_ctx, layout, oracle):
+def test_device_resident_api(fresh_ctx, layout, oracle):
     """msw_align_batch_device over HBM-resident arrays (the bench path)."""
     import torch
     b = config_batch(2, n_pairs=4000, seed_offset=77)
@@ -377,7 +377,7 @@ def test_device_resident_api(gpu_ctx, layout, oracle):
     ei = torch.zeros(b.n_pairs, dtype=torch.int16, device=dev)
     ej = torch.zeros(b.n_pairs, dtype=torch.int16, device=dev)
     sc = Scoring(want_coords=True)
-    gpu_ctx.align_batch_device(t["reads"].data_ptr(), rl.data_ptr(), t["wins"].data_ptr(), wl.data_ptr(),
+    fresh_ctx.align_batch_device(t["reads"].data_ptr(), rl.data_ptr(), t["wins"].data_ptr(), wl.data_ptr(),
                                b.reads.shape[1], b.wins.shape[1], b.n_pairs, score.data_ptr(),
                                int(b.read_len.max()), int(b.win_len.max()), sc, ei.data_ptr(),
                                ej.data_ptr(), torch.cuda.current_stream().cuda_stream)
@@ -417,7 +417,7 @@ def _planned(gpu_ctx, b, sc, passes=1):
 @pytest.mark.parametrize("sc", [Scoring(), Scoring(want_coords=True), Scoring(gap_open=3, gap_extend=1, affine=True),
                                 Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)],
                          ids=["linear", "linear+coords", "affine", "affine+coords"])
-def test_planned_mixed_lengths(gpu_ctx, oracle, monkeypatch, sc, multi):
+def test_planned_mixed_lengths(fresh_ctx, oracle, monkeypatch, sc, multi):
     """msw_plan_create + msw_align_batch_planned (config 5 shape, unsorted,
     device-resident): one length-bucketed launch (multi) or the single-bucket
     path over the plan's order (MSW_NO_MULTI), twice over the same plan."""
@@ -426,7 +426,7 @@ def test_planned_mixed_lengths(gpu_ctx, oracle, monkeypatch, sc, multi):
     if not multi:
         monkeypatch.setenv("MSW_NO_MULTI", "1")
     b = config_batch(5, n_pairs=9_000, seed_offset=31)
-    assert_same(_planned(gpu_ctx, b, sc, passes=2), oracle_run(oracle, b, sc), sc.want_coords)
+    assert_same(_planned(fresh_ctx, b, sc, passes=2), oracle_run(oracle, b, sc), sc.want_coords)
 
 
 def test_planned_edge_cases(gpu_ctx, oracle, monkeypatch):
@@ -533,16 +533,11 @@ def test_ctx_prepare_then_score(gpu_ctx, oracle):
 @pytest.mark.parametrize("nbytes,src_off,dst_off", [(1, 0, 0), (15, 0, 0), (4096 * 3 + 7, 0, 0), (1 << 20, 0, 0),
                                                     (100_003, 4, 4), (65_536, 3, 7), (262_144 * 2, 16, 0)])
 @pytest.mark.parametrize("pinned", [True, False])
-@pytest.mark.parametrize("dma", [False, True])
-def test_memcpy_d2h_async(gpu_ctx, monkeypatch, nbytes, src_off, dst_off, pinned, dma):
+def test_memcpy_d2h_async(gpu_ctx, nbytes, src_off, dst_off, pinned):
     """msw_memcpy_d2h_async: into pinned memory a copy kernel on the stream
-    (vector body when source and destination share their alignment mod 16,
-    bytes otherwise) or, with MSW_D2H_DMA=1, a DMA; into pageable memory a
-    DMA; all followed by a fence."""
-    if dma:
-        monkeypatch.setenv("MSW_D2H_DMA", "1")
-    else:
-        monkeypatch.delenv("MSW_D2H_DMA", raising=False)
+    when source and destination share their alignment mod 16, a DMA when they
+    do not (no byte-by-byte stores over PCIe); into pageable
+    memory a DMA; all followed by a fence."""
     import ctypes
     from mini_parallel_amd._lib import check, lib
     from mini_parallel_amd.aligner import pinned_empty
@@ -565,14 +560,12 @@ def test_memcpy_d2h_async(gpu_ctx, monkeypatch, nbytes, src_off, dst_off, pinned
         L.msw_dev_free(gpu_ctx.handle, d)
 
 
-@pytest.mark.parametrize("ramp", ["1", "0"])
-@pytest.mark.parametrize("chunk", [20_000, 65_536, 70_000])
-def test_chunk_ramp(gpu_ctx, oracle, monkeypatch, ramp, chunk):
+@pytest.mark.parametrize("chunk", [20_000, 65_536, 70_000, 131_072])
+def test_chunk_ramp(gpu_ctx, oracle, chunk):
     """A multi-chunk call: a short first chunk, then (chunk_pairs > 64k)
-    chunks doubling up to chunk_pairs, or (MSW_CHUNK_RAMP=0, smaller chunks)
-    the rest full size -- 100k config-3 pairs, affine + best cell, pairs
-    arrays and genome form, every pair against the SIMD oracle."""
-    monkeypatch.setenv("MSW_CHUNK_RAMP", ramp)
+    chunks doubling up to chunk_pairs, or (smaller chunks) the rest full size
+    -- 100k config-3 pairs, affine + best cell, pairs arrays and genome form,
+    every pair against the SIMD oracle."""
     b = config_batch(3, n_pairs=100_000, seed_offset=77)
     sc = Scoring(gap_open=3, gap_extend=1, affine=True, want_coords=True)
     want = oracle_run(oracle, b, sc)
@@ -585,3 +578,49 @@ def test_chunk_ramp(gpu_ctx, oracle, monkeypatch, ramp, chunk):
     finally:
         g.close()
     assert_same(got, want, True)
+
+
+def _trace_line(capfd):
+    return [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")][-1]
+
+
+def _cache_counts(line):
+    c = line.split("pinned_cache(")[1].split(")")[0]
+    return int(c.split("hits=")[1].split()[0]), int(c.split("misses=")[1].split()[0])
+
+
+def test_pinned_cache_lru_and_invalidation(fresh_ctx, oracle, monkeypatch, capfd):
+    """the pinned-range cache is LRU over 16 ranges, so six pinned
+    batches used in rotation (twelve ranges: reads and windows) all hit after
+    the first round -- the 8-entry FIFO it replaces missed every one -- and
+    msw_host_free empties it (a freed block's address may come back as
+    pageable memory).  Results stay bit-exact throughout."""
+    from mini_parallel_amd.aligner import pinned_empty
+    monkeypatch.setenv("MSW_HOST_TRACE", "1")
+    sc = Scoring()
+    batches = []
+    for k in range(6):
+        b = config_batch(2, n_pairs=500, seed_offset=300 + k)
+        pr, pw = pinned_empty(b.reads.shape, np.uint8), pinned_empty(b.wins.shape, np.uint8)
+        pr[...] = b.reads
+        pw[...] = b.wins
+        batches.append((B(pr, b.read_len, pw, b.win_len), oracle_run(oracle, b, sc)))
+    import gc
+    gc.collect()  # no other test's pinned array freed (cache emptied) mid-test
+    capfd.readouterr()
+    for b, want in batches:  # first round: every range is new
+        assert_same(gpu_run(fresh_ctx, b, sc), want, False)
+    h0, m0 = _cache_counts(_trace_line(capfd))
+    for b, want in batches * 2:  # later rounds: all hits
+        assert_same(gpu_run(fresh_ctx, b, sc), want, False)
+        assert "direct(reads=1 wins=1" in _trace_line(capfd)
+    gpu_run(fresh_ctx, batches[0][0], sc)
+    h1, m1 = _cache_counts(_trace_line(capfd))
+    assert m1 == m0 and h1 - h0 == 2 * 12 + 2, (h0, m0, h1, m1)
+    # any msw_host_free: the next lookups miss, and re-learn the ranges
+    junk = pinned_empty(4096, np.uint8)
+    del junk
+    gc.collect()
+    assert_same(gpu_run(fresh_ctx, batches[1][0], sc), batches[1][1], False)
+    h2, m2 = _cache_counts(_trace_line(capfd))
+    assert m2 == m1 + 2 and h2 == h1, (h1, m1, h2, m2)

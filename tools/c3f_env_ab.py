@@ -14,6 +14,7 @@ import os
 import subprocess
 import sys
 import tempfile
+import time
 
 import numpy as np
 
@@ -27,8 +28,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     ap.add_argument("--setting", action="append", required=True,
-                    help="NAME=VAR=VALUE[,VAR=VALUE...] (NAME= for no change)")
+                    help="NAME=VAR=VALUE[,VAR=VALUE...] (NAME= for no change; CLI=path runs another build "
+                         "of rustseq_mini, relative to the repo)")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--sleep", type=float, default=0.0, help="seconds idle before each run (lets the previous "
+                    "process's GPU teardown finish in the kernel)")
     ap.add_argument("--dir", default="/tmp/msw_bench_c4")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
@@ -49,16 +53,26 @@ def main():
         for rep in range(a.reps):
             for name, extra in settings:
                 wd = tempfile.mkdtemp(prefix="c3fab_")
+                extra = dict(extra)
+                exe = os.path.join(ROOT, extra.pop("CLI")) if "CLI" in extra else cli
                 env = dict(os.environ, WGS_DATA_DIR=d, WGS_SAMPLE_ID="SYN", WGS_LANES="1",
                            WGS_READS_PER_LANE=str(bench.C3F_RPL), GPU_CHUNK_SIZE_READS="65536",
                            WGS_RUN_ID=f"c3fab_{name}_{rep}", **extra)
-                cmd = [cli, "--full-wgs", "--gpu", "--score-mode", "sw", "--reference", os.path.join(d, "reference.fa"),
+                cmd = [exe, "--full-wgs", "--gpu", "--score-mode", "sw", "--reference", os.path.join(d, "reference.fa"),
                        "--window", str(bench.C4_WINDOW), "--checkpoint-dir", wd, "--json", os.path.join(wd, "rec.json"),
                        "--num-gpus", "1", "--gap-model", "affine", "--scores-out", wd]
+                time.sleep(a.sleep)
+                t0 = time.perf_counter()
+                t_launch = time.time_ns()
                 r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+                t_end = time.time_ns()
+                proc_ms = (time.perf_counter() - t0) * 1e3
                 if r.returncode:
                     raise SystemExit(f"{name} rep {rep}: rc {r.returncode}\n{r.stderr[-3000:]}")
                 rec = json.load(open(os.path.join(wd, "rec.json")))
+                tm, tr = rec.get("t_main_unix_ns"), rec.get("t_record_unix_ns")
+                phases = {"start_ms": round((tm - t_launch) * 1e-6, 1), "main_to_record_ms": round((tr - tm) * 1e-6, 1),
+                          "exit_ms": round((t_end - tr) * 1e-6, 1)} if tm and tr else None
                 bad = 0
                 for base, (s, i, j) in want.items():
                     g = np.fromfile(os.path.join(wd, base + ".scores"), dtype=[("s", "<i4"), ("i", "<i2"), ("j", "<i2")])
@@ -68,7 +82,9 @@ def main():
                        "setup_ms": round(rec["setup_ms"], 1),
                        "reads_per_s": round(rec["total_reads"] / (rec["wall_ms"] * 1e-3)),
                        "reads_per_s_incl_setup": round(rec["total_reads"] / ((rec["wall_ms"] + rec["setup_ms"]) * 1e-3)),
-                       "kernel_ms": rec.get("kernel_ms"), "mismatches": bad}
+                       "kernel_ms": rec.get("kernel_ms"), "teardown_ms": rec.get("teardown_ms"),
+                       "process_wall_ms": round(proc_ms, 1), "setup_phases": rec.get("setup_phases"),
+                       "process_phases": phases, "mismatches": bad}
                 out.write(json.dumps(row) + "\n")
                 out.flush()
                 print(json.dumps(row), flush=True)

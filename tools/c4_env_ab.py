@@ -3,7 +3,7 @@
 bench.py's full-size config-4 lane set, runs alternating (every run's
 per-file sums checked against the oracle, tools/c4_full.run_cli):
 
-  python3 tools/c4_env_ab.py --b MSW_GENOME_CUT=1 --out gpurun_out/T/ab.jsonl [--reps 3]
+  python3 tools/c4_env_ab.py --b MSW_GFASTQ_BATCH=524288 --out gpurun_out/T/ab.jsonl [--reps 3]
 """
 import argparse
 import json

@@ -4,9 +4,8 @@ host_to_host leg, genome_pinned form): 1 M pairs of 150 x 300, affine + best
 cell, reads + window positions in pinned host memory, the windows' genome
 resident in HBM, chunked async H2D / kernels / readback through
 msw_align_reads; best of 3 per chunk size, checked against one HBM-resident
-run.  One JSON line per chunk size (and per --ramp setting: MSW_CHUNK_RAMP
-values alternated within each chunk size, `--reps` rounds).
-  python3 tools/h2h_sweep.py --chunks 32768,65536,131072,262144 [--ramp 1,0] > out.jsonl"""
+run.  One JSON line per chunk size and round (`--reps`).
+  python3 tools/h2h_sweep.py --chunks 32768,65536,131072,262144 > out.jsonl"""
 import argparse
 import json
 import os
@@ -21,7 +20,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", default="32768,65536,131072,262144,524288")
     ap.add_argument("--pairs", type=int, default=1_000_000)
-    ap.add_argument("--ramp", default="1", help="MSW_CHUNK_RAMP settings to alternate")
     ap.add_argument("--reps", type=int, default=1)
     args = ap.parse_args()
     import numpy as np
@@ -45,8 +43,7 @@ def main():
     want = ctx.align_reads(genome, reads, rl, pos, wl, scoring=AFFINE, chunk_pairs=b.n_pairs)
     for rep in range(args.reps):
         for chunk in [int(x) for x in args.chunks.split(",")]:
-            for ramp in args.ramp.split(","):
-                os.environ["MSW_CHUNK_RAMP"] = ramp
+            for _ in (0,):
                 got = ctx.align_reads(genome, reads, rl, pos, wl, scoring=AFFINE, chunk_pairs=chunk)
                 ok = all(np.array_equal(g, w) for g, w in zip(got, want))
                 best = 1e30
@@ -55,7 +52,7 @@ def main():
                     t0 = time.perf_counter()
                     ctx.align_reads(genome, reads, rl, pos, wl, scoring=AFFINE, chunk_pairs=chunk)
                     best = min(best, time.perf_counter() - t0)
-                print(json.dumps({"chunk_pairs": chunk, "ramp": ramp, "rep": rep, "ms": round(best * 1e3, 3),
+                print(json.dumps({"chunk_pairs": chunk, "rep": rep, "ms": round(best * 1e3, 3),
                                   "gcups": round(b.cells / best / 1e9, 1), "bit_exact": ok}), flush=True)
     genome.close()
     ctx.close()

@@ -4,7 +4,7 @@ pcie_inclusive.genome_pinned_stream: pinned reads + positions against an
 HBM-resident genome, three in flight) under environment settings read per
 call by the library, alternated --reps times after a preheat; every run's
 last scores checked.  One JSON line per run.
-  python3 tools/stream_ab.py --setting base= --setting one=MSW_ASYNC_ONE_STREAM=1"""
+  python3 tools/stream_ab.py --setting base= --setting other=VAR=VALUE"""
 import argparse
 import json
 import os
