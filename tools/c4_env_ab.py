@@ -4,6 +4,7 @@ bench.py's full-size config-4 lane set, runs alternating (every run's
 per-file sums checked against the oracle, tools/c4_full.run_cli):
 
   python3 tools/c4_env_ab.py --b MSW_GFASTQ_BATCH=524288 --out gpurun_out/T/ab.jsonl [--reps 3]
+  python3 tools/c4_env_ab.py --cli-b tools/bin/VARIANT/rustseq_mini --out ...
 """
 import argparse
 import json
@@ -20,7 +21,8 @@ from c4_full import run_cli  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--b", action="append", required=True, help="NAME=VALUE set for the b runs (repeatable)")
+    ap.add_argument("--b", action="append", default=[], help="NAME=VALUE set for the b runs (repeatable)")
+    ap.add_argument("--cli-b", default=None, help="another rustseq_mini build for the b runs (repo-relative)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--dir", default="/tmp/msw_bench_c4")
     ap.add_argument("--out", required=True)
@@ -38,7 +40,8 @@ def main():
                 if tag == "b":
                     os.environ.update(env_b)
                 try:
-                    row = run_cli(d, files, "1", f"{tag}_{rep}", out_dir)
+                    row = run_cli(d, files, "1", f"{tag}_{rep}", out_dir,
+                                  cli=os.path.join(ROOT, a.cli_b) if tag == "b" and a.cli_b else None)
                 finally:
                     for k, v in saved.items():
                         if v is None:
@@ -46,6 +49,7 @@ def main():
                         else:
                             os.environ[k] = v
                 row["env"] = env_b if tag == "b" else {}
+                row["cli"] = a.cli_b if tag == "b" and a.cli_b else "in-tree"
                 f.write(json.dumps(row) + "\n")
                 f.flush()
                 print(f"[c4_env_ab] {tag} rep {rep}: {row['reads_per_second'] / 1e6:.1f} M reads/s, "
