@@ -100,6 +100,17 @@ int msw_device_info(int ordinal, msw_device_info_t* out);
  * compute, copy and readback streams and three pinned staging slots (up to
  * three chunks in flight). */
 int msw_ctx_create(int ordinal, msw_ctx** out);
+/* msw_ctx_create with flags.  MSW_CTX_LEAN: only the compute stream up
+ * front; the copy / second compute / readback / side streams are made by the
+ * first call that needs them (host-batch calls, long pairs beside packed
+ * ones).  A stream costs 3-30 ms to create -- the first few of a process each
+ * make a hardware queue -- and the --full-wgs GPU-reader workers, which
+ * score device-resident batches only, never use them.  Without the flag all
+ * five streams are made here, before any the caller creates, so they land
+ * on their own hardware queues.  The library reads its environment switches
+ *  once, here. */
+#define MSW_CTX_LEAN 1u
+int msw_ctx_create_ex(int ordinal, unsigned flags, msw_ctx** out);
 void msw_ctx_destroy(msw_ctx* ctx);
 
 /* Batched scoring from host memory, synchronous.  Streams the batch through

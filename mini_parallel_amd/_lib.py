@@ -22,7 +22,7 @@ MSW_E_NOMEM = -5
 
 # Every symbol include/msw.h declares (checked by tests/test_abi.py).
 EXPORTED = (
-    "msw_device_count", "msw_device_info", "msw_ctx_create", "msw_ctx_destroy",
+    "msw_device_count", "msw_device_info", "msw_ctx_create", "msw_ctx_create_ex", "msw_ctx_destroy",
     "msw_align_batch", "msw_align_batch_async", "msw_wait", "msw_align_batch_device",
     "msw_align_compat", "msw_host_alloc", "msw_host_free", "msw_dev_alloc", "msw_dev_free",
     "msw_memcpy_h2d", "msw_memcpy_d2h", "msw_synchronize", "msw_last_error", "msw_version",
@@ -97,6 +97,7 @@ def _declare(L):
         "msw_device_count": (I, [ctypes.POINTER(I)]),
         "msw_device_info": (I, [I, ctypes.POINTER(DeviceInfoT)]),
         "msw_ctx_create": (I, [I, ctypes.POINTER(P)]),
+        "msw_ctx_create_ex": (I, [I, ctypes.c_uint, ctypes.POINTER(P)]),
         "msw_ctx_destroy": (None, [P]),
         "msw_align_batch": (I, [P, ctypes.POINTER(ScoringT), ctypes.POINTER(BatchT),
                                 ctypes.POINTER(OutT), ctypes.c_uint64]),

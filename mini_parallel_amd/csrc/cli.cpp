@@ -237,8 +237,8 @@ struct Ctx {
     // checkpoint are written, so releasing them one by one (50-60 ms of
     // unregisters and frees after the last results) is work the OS redoes
     bool keep = false;
-    explicit Ctx(int ordinal) {
-        if (msw_ctx_create(ordinal, &h) != MSW_OK) die(std::string("GPU context error: ") + msw_last_error());
+    explicit Ctx(int ordinal, unsigned flags = 0) {
+        if (msw_ctx_create_ex(ordinal, flags, &h) != MSW_OK) die(std::string("GPU context error: ") + msw_last_error());
     }
     ~Ctx() {
         if (!keep) msw_ctx_destroy(h);
@@ -789,31 +789,14 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
             workers.emplace_back([&, wi]() {
                 const int gi = wi % ngpu;
                 const auto ts0 = Clock::now();
-                Ctx ctx(devices[gi].ordinal);
+                // lean: a GPU-reader worker scores device-resident batches
+                // only, so its context makes just the compute stream
+                Ctx ctx(devices[gi].ordinal, MSW_CTX_LEAN);
                 const double t_ctx = ms_since(ts0);
-                const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
-                // Setup after the context runs on two threads: the genome
-                // upload (copy stream) and the scoring kernels' module loads
-                // on a helper, beside the lane reader's buffers and the result
-                // sets here (each ~15-40 ms; in sequence they were the bulk of
-                // setup_ms, profiles/r06/c3f/).
-                msw_genome* gen = nullptr;
-                double t_gen = 0, t_kl = 0;
-                std::thread helper([&]() {
-                    const auto th0 = Clock::now();
-                    const std::string& ref_seq = genome();
-                    if (msw_genome_create(ctx.h, (const uint8_t*)ref_seq.data(), ref_seq.size(), &gen) != MSW_OK)
-                        die(std::string("GPU genome upload error: ") + msw_last_error());
-                    t_gen = ms_since(th0);
-                    // the scoring kernels' modules, loaded now rather than at the first batch
-                    if (msw_ctx_prepare(ctx.h, &sc) != MSW_OK) die(std::string("GPU kernel load: ") + msw_last_error());
-                    t_kl = ms_since(th0) - t_gen;
-                });
-                const auto tr0 = Clock::now();
                 msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
                 if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
                     die(std::string("GPU lane reader: ") + msw_last_error());
-                const double t_rd = ms_since(tr0);
+                const double t_rd = ms_since(ts0) - t_ctx;
                 const size_t kNone = ~(size_t)0;
                 size_t pending = kNone;
                 auto claim = [&]() -> size_t {
@@ -822,10 +805,24 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 };
                 // the first file: claimed now and opened / pinned on the
                 // reader's thread (msw_gfastq_prefetch) while this worker
-                // allocates its result sets and the helper uploads the
-                // genome, so its first window is ready when the clock starts
+                // uploads the genome and allocates its result sets, so its
+                // first window is ready when the clock starts (the same work
+                // on a helper thread beside the reader's buffers measured
+                // equal, and starting the prefetch later cost ~0.5 ms of the
+                // timed region: profiles/r06/c3f/setup_ab.jsonl)
                 pending = claim();
                 if (pending != kNone) (void)msw_gfastq_prefetch(gr, st[pending]->path.c_str());
+                const msw_scoring_t sc = scoring_of(a, !a.scores_out.empty());
+                msw_genome* gen = nullptr;
+                const auto tg0 = Clock::now();
+                const std::string& ref_seq = genome();
+                if (msw_genome_create(ctx.h, (const uint8_t*)ref_seq.data(), ref_seq.size(), &gen) != MSW_OK)
+                    die(std::string("GPU genome upload error: ") + msw_last_error());
+                const double t_gen = ms_since(tg0);
+                // the scoring kernels' modules, loaded now rather than at the first batch
+                const auto tk0 = Clock::now();
+                if (msw_ctx_prepare(ctx.h, &sc) != MSW_OK) die(std::string("GPU kernel load: ") + msw_last_error());
+                const double t_kl = ms_since(tk0);
                 const auto tres0 = Clock::now();
                 // two result sets: batch k's copy-back lands while batch k+1 runs
                 struct Res {
@@ -849,7 +846,6 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                         die(std::string("GPU lane reader buffers: ") + msw_last_error());
                 }
                 const double t_res = ms_since(tres0);
-                helper.join();
                 unsigned long long alg_local = 0;
                 // per file this worker has open: batches in flight, reader done
                 std::map<size_t, std::pair<int, bool>> open_files;
@@ -1480,8 +1476,12 @@ int main(int argc, char** argv) {
         // Records, scores files and checkpoint are written and closed: end the
         // process here.  The workers' contexts, genomes and pinned buffers are
         // released by the exit itself (Ctx::keep), not call by call.
+        // Under rocprofv3 (its tool library is named in the environment) the
+        // ordinary exit runs, so the profiler's exit handlers write its
+        // output; the contexts are still left to the runtime's own exit.
         fflush(stdout);
         fflush(stderr);
+        if (getenv("ROCP_TOOL_LIBRARIES") || getenv("ROCPROF_OUTPUT_PATH")) exit(all_ok ? 0 : 1);
         _exit(all_ok ? 0 : 1);
     }
 

@@ -64,12 +64,6 @@ constexpr uint64_t kPad = 256;             // device buffers: slack past the end
 constexpr uint64_t kReadPiece = 8u << 20;  // compressed bytes per fread
 constexpr uint64_t kInPad = 1024;          // past the compressed bytes: the inflate input window reads <= 520 B
 constexpr uint64_t kDefaultSpan = 1024u << 20;  // ~16k members: two rounds of 8 inflate waves per SIMD
-// A file's first span inflates as two member groups (inflate-ahead): the
-// first group's lines are parsed and handed out as batches while the second
-// group inflates, so scoring starts after half a span's inflate instead of a
-// whole one.  Spans of fewer members inflate in one launch.
-constexpr bool kSplitFirstSpan = true;
-constexpr size_t kSplitMinMembers = 64;
 
 const char* status_text(uint32_t s) {
     switch (s) {
@@ -198,11 +192,6 @@ struct Inflater {
         d_crc = nullptr;
         h_flag = nullptr;
     }
-    // The compressed source and member count of the group launches (begin).
-    const uint8_t* src = nullptr;
-    size_t src_bytes = 0;
-    uint32_t n_members = 0;
-
     // upload cbytes of compressed data + the member table, inflate into out,
     // check CRCs.  in_place: the device address of h_comp's pinned pages --
     // the kernel then reads the compressed bytes over PCIe as it decodes
@@ -210,18 +199,10 @@ struct Inflater {
     int run(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, uint8_t* out,
             hipStream_t s, const uint8_t* in_place = nullptr) {
         int rc;
-        if ((rc = begin(h_comp, cbytes, mem, s, in_place))) return rc;
-        return group(0, (uint32_t)mem.size(), 0, out, s);
-    }
-    // the upload (or in-place source) and the member table of a span, and
-    // both groups' error flags cleared
-    int begin(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, hipStream_t s,
-              const uint8_t* in_place) {
-        int rc;
         if ((rc = grow(&d_mem, &mem_cap, mem.size()))) return rc;
         if ((rc = grow(&d_status, &status_cap, mem.size()))) return rc;
-        src = in_place;
-        src_bytes = cbytes;
+        const uint8_t* src = in_place;
+        size_t src_bytes = cbytes;
         if (!src) {
             if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
             if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
@@ -229,17 +210,10 @@ struct Inflater {
             src = dc;
             src_bytes = cbytes + kInPad;
         }
-        n_members = (uint32_t)mem.size();
         if (!mem.empty())
             GZ_TRY(hipMemcpyAsync(d_mem, mem.data(), mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
-        GZ_TRY(hipMemsetAsync(d_flag, 0, 8, s));
-        return MSW_OK;
-    }
-    // inflate + CRC of members [first, first + n) of the span begun; their
-    // error flag is word `fl` (0 or 1) of d_flag / h_flag
-    int group(uint32_t first, uint32_t n, int fl, uint8_t* out, hipStream_t s) {
-        const msw::GzMember* gm = d_mem + first;
-        uint32_t* gst = d_status + first;
+        GZ_TRY(hipMemsetAsync(d_flag, 0, 4, s));
+        const uint32_t n = (uint32_t)mem.size();
         static const bool timing = getenv("MSW_GZ_TIMING") != nullptr;  // kernel times to stderr (tools)
         if (timing) {
             if (!ev[0]) {
@@ -253,7 +227,7 @@ struct Inflater {
         uint32_t* d_prof = nullptr;
         if (prof_on && n) GZ_TRY(hipMalloc((void**)&d_prof, (size_t)n * 64));
         if (d_prof) GZ_TRY(hipMemsetAsync(d_prof, 0, (size_t)n * 64, s));
-        GZ_TRY(msw::launch_gz_inflate(src, src_bytes, gm, n, out, gst, d_flag + fl, s, d_prof));
+        GZ_TRY(msw::launch_gz_inflate(src, src_bytes, d_mem, n, out, d_status, d_flag, s, d_prof));
         if (timing) GZ_TRY(hipEventRecord(ev[1], s));
         if (d_prof) {
             std::vector<uint32_t> h((size_t)n * 16);
@@ -270,30 +244,29 @@ struct Inflater {
             fprintf(stderr, "\n");
             (void)hipFree(d_prof);
         }
-        GZ_TRY(msw::launch_gz_crc(out, gm, n, d_crc, gst, d_flag + fl, s));
+        GZ_TRY(msw::launch_gz_crc(out, d_mem, n, d_crc, d_status, d_flag, s));
         if (timing) {
             GZ_TRY(hipEventRecord(ev[2], s));
             GZ_TRY(hipEventSynchronize(ev[2]));
             float a = 0, c = 0;
             (void)hipEventElapsedTime(&a, ev[0], ev[1]);
             (void)hipEventElapsedTime(&c, ev[1], ev[2]);
-            fprintf(stderr, "[gz] %u members (from %u), %zu B in: inflate %.3f ms, crc %.3f ms\n", n, first,
-                    src_bytes, a, c);
+            uint64_t ob = 0;
+            for (const auto& m : mem) ob += m.isize;
+            fprintf(stderr, "[gz] %u members, %zu B in, %llu B out: inflate %.3f ms (%.2f GB/s out), crc %.3f ms\n", n,
+                    cbytes, (unsigned long long)ob, a, ob / (a * 1e6), c);
         }
-        GZ_TRY(hipMemcpyAsync(h_flag + fl, d_flag + fl, 4, hipMemcpyDeviceToHost, s));
+        GZ_TRY(hipMemcpyAsync(h_flag, d_flag, 4, hipMemcpyDeviceToHost, s));
         return MSW_OK;
     }
-    // after the group's flag copy completed: error message for the first
-    // failing member of [first, first + n)
-    int check(const std::vector<msw::GzMember>& mem, const char* what, uint32_t first = 0, uint32_t n = ~0u,
-              int fl = 0) {
-        if (!h_flag[fl]) return MSW_OK;
-        n = std::min<uint32_t>(n, (uint32_t)mem.size() - first);
-        std::vector<uint32_t> st(n);
-        GZ_TRY(hipMemcpy(st.data(), d_status + first, st.size() * 4, hipMemcpyDeviceToHost));
+    // after the stream synchronised: error message for the first failing member
+    int check(const std::vector<msw::GzMember>& mem, const char* what) {
+        if (!h_flag[0]) return MSW_OK;
+        std::vector<uint32_t> st(mem.size());
+        GZ_TRY(hipMemcpy(st.data(), d_status, st.size() * 4, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < st.size(); ++i)
             if (st[i]) return set_error(MSW_E_INVALID, "Error reading %s: %s (BGZF member %zu of the span)", what,
-                                        status_text(st[i]), first + i);
+                                        status_text(st[i]), i);
         return set_error(MSW_E_INVALID, "Error reading %s: invalid compressed data", what);
     }
 };
@@ -308,29 +281,14 @@ struct msw_gfastq {
     uint64_t in_place_max = 64ull << 20;  // MSW_GZ_IN_PLACE_MB: first spans up to this are inflated in place
     bool no_map = false;               // MSW_GZ_NO_MAP=1: copied mode (preads into pinned staging)
     hipStream_t rs = nullptr;          // the reader's own stream (inflate + parse)
-    hipEvent_t parsed = nullptr;       // phase B of the current part done
-    // per span buffer i (dout[i]): the last emit that read it, on the
-    // caller's stream.  A span only waits for the emits of the span two
-    // before it, so inflating and parsing the next span (or the next file)
-    // runs beside the current span's emits and scoring.
+    hipEvent_t parsed = nullptr;       // phase B of the current span done
+    // per span buffer i (dout[i] and its line arrays pb[i]): the last emit
+    // that read it, on the caller's stream.  A span only waits for the emits
+    // of the span two before it, so inflating and parsing the next span (or
+    // the next file) runs beside the current span's emits and scoring.
     hipEvent_t emitted[2] = {nullptr, nullptr};
     bool emitted_valid[2] = {false, false};
-    // per parse-array slot s (pb[s]): the last emit that read its line
-    // arrays.  Slots alternate per parsed part (a span is one part, or two
-    // when it inflates as two member groups), buffers per span.
-    hipEvent_t lines_emitted[2] = {nullptr, nullptr};
-    bool lines_emitted_valid[2] = {false, false};
-    int next_pb = 0;                   // slot of the next part
-    int cur_pb = 0;                    // slot of the current part
     int last_buf = 1;                  // buffer of the latest span (any file); the next takes the other
-    // A span inflated as two member groups: group 2 was launched after part
-    // 1's parse; part 2 (its lines) is parsed at the next next_span call.
-    bool part2 = false;
-    uint32_t g2_first = 0;             // first member of group 2
-    uint64_t g1_out = 0;               // output bytes of group 1 (from kCarry)
-    uint64_t span_obytes = 0;          // output bytes of the whole span
-    size_t span_used = 0;              // its compressed bytes
-    bool span_last = false;            // it ends the file
     FILE* f = nullptr;
     std::string path;
     uint64_t fsize = 0, fread_off = 0;
@@ -484,8 +442,6 @@ void release(msw_gfastq* g) {
     if (g->parsed) (void)hipEventDestroy(g->parsed);
     for (hipEvent_t e : g->emitted)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : g->lines_emitted)
-        if (e) (void)hipEventDestroy(e);
     if (g->rs) (void)hipStreamDestroy(g->rs);
     delete g;
 }
@@ -621,143 +577,7 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Phase A over b (its window set by the caller): line counts back on the
-// host.  Synchronises the reader stream.
-int parse_a(msw_gfastq* g, msw::ParseBufs& b, hipStream_t s) {
-    int rc;
-    b.want_pos = g->want_pos ? 1u : 0u;
-    b.ntiles = (uint32_t)((b.len + msw::kParseTile - 1) / msw::kParseTile);
-    if ((rc = grow(&g->tile_nl, &g->tile_cap, (size_t)b.ntiles + 1))) return rc;
-    if ((rc = grow(&g->tile_hi, &g->tile_hi_cap, (size_t)b.ntiles + 1))) return rc;
-    b.tile_nl = g->tile_nl;
-    b.tile_hi = g->tile_hi;
-    b.line_cap = ~0ull;
-    b.state = g->d_state;
-    b.out = g->d_out;
-    b.stride = g->stride;
-    GZ_TRY(msw::launch_parse_a(b, s));
-    GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
-    GZ_TRY(hipStreamSynchronize(s));
-    return MSW_OK;
-}
-
-// Phase B of the part in parse slot `slot` (line arrays sized from phase A's
-// counts), its results copied back and `parsed` recorded; `then` enqueues
-// more reader work behind it before the host waits (group 2's inflate).
-template <typename Then>
-int parse_b(msw_gfastq* g, int slot, hipStream_t s, Then then) {
-    int rc;
-    msw::ParseBufs& b = g->pb[slot];
-    const uint64_t nlines = g->h_out->lines;
-    const bool any_high = g->h_out->any_high != 0;
-    if ((rc = grow(&b.line_end, &g->line_cap[slot], (size_t)nlines + 1))) return rc;
-    b.line_cap = g->line_cap[slot];
-    if (any_high) {
-        if ((rc = grow(&b.vidx, &g->vidx_cap[slot], (size_t)nlines + 1))) return rc;
-        if ((rc = grow(&b.vline, &g->v_cap[slot], (size_t)nlines + 1))) return rc;
-        if ((rc = grow(&b.blk, &g->blk_cap[slot], (size_t)(nlines / 1024 + 2)))) return rc;
-    }
-    // read-length maxima per run of whole batches (<= kLenBuckets runs)
-    {
-        const uint64_t batches = (nlines / 4 + 1 + g->max_reads - 1) / g->max_reads;
-        b.bucket_reads = g->max_reads * ((batches + msw::kLenBuckets - 1) / msw::kLenBuckets);
-    }
-    GZ_TRY(msw::launch_parse_b(b, nlines, any_high, s));
-    GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
-    GZ_TRY(hipEventRecord(g->parsed, s));
-    if ((rc = then())) return rc;
-    GZ_TRY(hipEventSynchronize(g->parsed));
-    return MSW_OK;
-}
-
-// The parsed part becomes the current one: its reads are what
-// msw_gfastq_next hands out next.
-int adopt_part(msw_gfastq* g, int buf, int slot, bool last) {
-    const msw::ParseOut& o = *g->h_out;
-    const msw::ParseBufs& b = g->pb[slot];
-    if (o.err_over)
-        return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
-                         (unsigned long long)o.err_line);
-    if (o.too_long)
-        return set_error(MSW_E_RANGE, "sequence longer than the slab stride %u at line %llu", g->stride,
-                         (unsigned long long)o.too_long_line);
-    g->cur = buf;
-    g->cur_pb = slot;
-    g->last_buf = buf;
-    g->cur_off = (uint64_t)(b.buf - g->dout[buf]);
-    g->cur_len = b.len;
-    g->tail_start = o.tail_start;
-    g->started = true;
-    g->at_eof = last;
-    g->span_reads = o.reads;
-    g->span_done = 0;
-    g->span_min = o.min_len;
-    g->span_max = o.max_len;
-    g->bucket_reads = b.bucket_reads;
-    memcpy(g->span_bmax, o.bmax, sizeof(g->span_bmax));
-    g->sp.v0 = o.v0;
-    g->sp.pending_in = o.pending_in;
-    g->sp.any_high = o.any_high;
-    g->lines += o.valid;
-    g->errors += o.lines - o.valid;
-    g->reads += o.reads;
-    g->bases += o.bases;
-    return MSW_OK;
-}
-
-// After a span's inflate has finished reading its compressed bytes: drop
-// them (unpin the mapped window) and start reading ahead the next ones.
-void release_span_input(msw_gfastq* g, size_t used) {
-    if (g->mapped) {
-        // the window's upload is done: unpin it; the next one registers in the background
-        (void)hipHostUnregister(g->map + g->reg_lo);
-        g->reg_len = 0;
-        g->map_off += used;
-        g->hc_len = 0;
-    } else if (used) {
-        memmove(g->hc, g->hc + used, g->hc_len - used);
-        g->hc_len -= used;
-    }
-    g->last_used = used;
-    start_filler(g);
-}
-
-// The next parse slot, once the emits that read its line arrays are done
-// (on the reader stream).
-int take_slot(msw_gfastq* g, hipStream_t s, int* slot) {
-    const int k = g->next_pb;
-    g->next_pb ^= 1;
-    if (g->lines_emitted_valid[k]) GZ_TRY(hipStreamWaitEvent(s, g->lines_emitted[k], 0));
-    *slot = k;
-    return MSW_OK;
-}
-
-// Part 2 of a span inflated as two member groups: group 2's lines, parsed
-// from part 1's unfinished last line, which lies right before them in the
-// same buffer.
-int next_part2(msw_gfastq* g) {
-    int rc;
-    hipStream_t s = g->rs;
-    g->part2 = false;
-    int slot = 0;
-    if ((rc = take_slot(g, s, &slot))) return rc;
-    msw::ParseBufs& b = g->pb[slot];
-    const uint64_t from = g->cur_off + g->tail_start;  // part 1's unfinished line
-    const uint64_t base = from & ~(uint64_t)15;
-    b.buf = g->dout[g->cur] + base;
-    b.begin = (uint32_t)(from - base);
-    b.len = kCarry + g->span_obytes - base;
-    b.eof = g->span_last ? 1u : 0u;
-    if ((rc = parse_a(g, b, s))) return rc;  // behind group 2's inflate on the reader stream
-    if ((rc = g->inf.check(g->mem, g->path.c_str(), g->g2_first, ~0u, 1))) return rc;
-    release_span_input(g, g->span_used);
-    if ((rc = parse_b(g, slot, s, [] { return MSW_OK; }))) return rc;
-    g->bytes_out += g->span_obytes - g->g1_out;
-    return adopt_part(g, g->cur, slot, g->span_last);
-}
-
 int next_span(msw_gfastq* g) {
-    if (g->part2) return next_part2(g);
     int rc;
     static const bool trace = getenv("MSW_GFASTQ_TRACE") != nullptr;
     const double t0 = trace ? now_ms() : 0.0;
@@ -813,12 +633,10 @@ int next_span(msw_gfastq* g) {
 
     const double t_read = trace ? now_ms() : 0.0;
     hipStream_t s = g->rs;
-    // dout[nx] was last read by the emits of the span before the current one
-    // (long finished, normally); the current span's emits and the caller's
-    // scoring keep running
+    // dout[nx] and its line arrays were last read by the emits of the span
+    // before the current one (long finished, normally); the current span's
+    // emits and the caller's scoring keep running
     if (g->emitted_valid[nx]) GZ_TRY(hipStreamWaitEvent(s, g->emitted[nx], 0));
-    int slot = 0;
-    if ((rc = take_slot(g, s, &slot))) return rc;
     // 2. inflate + CRC into dout[nx] at kCarry (mapped: the upload starts at
     // the page boundary below hc, inside the registered window)
     const size_t lead = g->mapped ? (size_t)(g->map_off - g->reg_lo) : 0;
@@ -839,21 +657,7 @@ int next_span(msw_gfastq* g) {
         else
             (void)hipGetLastError();
     }
-    // A file's first span inflates as two member groups (kSplitFirstSpan):
-    // group 1 holds the members of the span's first half of output.
-    const uint32_t n_mem = (uint32_t)g->mem.size();
-    uint32_t m1 = n_mem;
-    uint64_t o1 = obytes;
-    if (kSplitFirstSpan && g->cur < 0 && n_mem >= kSplitMinMembers) {
-        uint64_t acc = 0;
-        m1 = 0;
-        while (m1 < n_mem && 2 * acc < obytes) acc += g->mem[m1++].isize;
-        o1 = acc;
-        if (m1 >= n_mem) m1 = n_mem, o1 = obytes;
-    }
-    const bool split = m1 < n_mem;
-    if ((rc = g->inf.begin(g->hc - lead, used + lead, g->mem, s, in_place))) return rc;
-    if ((rc = g->inf.group(0, m1, 0, g->dout[nx], s))) return rc;
+    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s, in_place))) return rc;
     // 3. the previous span's unfinished line goes right in front
     const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
     if (carry > kCarry)
@@ -862,43 +666,100 @@ int next_span(msw_gfastq* g) {
     if (carry)
         GZ_TRY(hipMemcpyAsync(g->dout[nx] + kCarry - carry, g->dout[g->cur] + g->cur_off + g->tail_start, carry,
                               hipMemcpyDeviceToDevice, s));
-    // 4. parse phase A over [kCarry - carry, kCarry + o1), from a 16-byte aligned base
-    msw::ParseBufs& b = g->pb[slot];
+    // 4. parse phase A over [kCarry - carry, kCarry + obytes), from a 16-byte aligned base
+    msw::ParseBufs& b = g->pb[nx];
     const uint64_t base = (kCarry - carry) & ~(uint64_t)15;
     b.buf = g->dout[nx] + base;
     b.begin = (uint32_t)(kCarry - carry - base);
-    b.len = kCarry + o1 - base;
-    b.eof = last && !split ? 1u : 0u;
-    if ((rc = parse_a(g, b, s))) return rc;
+    b.len = kCarry + obytes - base;
+    b.eof = last ? 1u : 0u;
+    b.want_pos = g->want_pos ? 1u : 0u;
+    b.ntiles = (uint32_t)((b.len + msw::kParseTile - 1) / msw::kParseTile);
+    if ((rc = grow(&g->tile_nl, &g->tile_cap, (size_t)b.ntiles + 1))) return rc;
+    if ((rc = grow(&g->tile_hi, &g->tile_hi_cap, (size_t)b.ntiles + 1))) return rc;
+    b.tile_nl = g->tile_nl;
+    b.tile_hi = g->tile_hi;
+    b.line_cap = ~0ull;
+    b.state = g->d_state;
+    b.out = g->d_out;
+    b.stride = g->stride;
+    GZ_TRY(msw::launch_parse_a(b, s));
+    GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
+    GZ_TRY(hipStreamSynchronize(s));
     const double t_a = trace ? now_ms() : 0.0;
-    if (lead)  // the member table is uploaded: it holds offsets into hc again
+    if (lead)  // uploads done: the member table holds offsets into hc again
         for (msw::GzMember& m : g->mem) m.coff -= lead;
-    if ((rc = g->inf.check(g->mem, g->path.c_str(), 0, m1, 0))) return rc;
-    // the upload of hc has completed (in place: group 2 still reads it)
-    if (!split) release_span_input(g, used);
+    if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
+    // the upload of hc has completed: drop the consumed bytes and read ahead
+    if (g->mapped) {
+        // the window's upload is done: unpin it; the next one registers in the background
+        (void)hipHostUnregister(g->map + g->reg_lo);
+        g->reg_len = 0;
+        g->map_off += used;
+        g->hc_len = 0;
+    } else if (used) {
+        memmove(g->hc, g->hc + used, g->hc_len - used);
+        g->hc_len -= used;
+    }
+    g->last_used = used;
+    start_filler(g);
     const double t_unpin = trace ? now_ms() : 0.0;
-    // 5. phase B; a split span's group 2 inflates behind it on the reader
-    // stream while the caller scores part 1's batches
-    if ((rc = parse_b(g, slot, s, [&]() { return split ? g->inf.group(m1, n_mem - m1, 1, g->dout[nx], s) : MSW_OK; })))
-        return rc;
+    const uint64_t nlines = g->h_out->lines;
+    const bool any_high = g->h_out->any_high != 0;
+    // 5. size the line arrays, phase B
+    if ((rc = grow(&b.line_end, &g->line_cap[nx], (size_t)nlines + 1))) return rc;
+    b.line_cap = g->line_cap[nx];
+    if (any_high) {
+        if ((rc = grow(&b.vidx, &g->vidx_cap[nx], (size_t)nlines + 1))) return rc;
+        if ((rc = grow(&b.vline, &g->v_cap[nx], (size_t)nlines + 1))) return rc;
+        if ((rc = grow(&b.blk, &g->blk_cap[nx], (size_t)(nlines / 1024 + 2)))) return rc;
+    }
+    // read-length maxima per run of whole batches (<= kLenBuckets runs)
+    {
+        const uint64_t batches = (nlines / 4 + 1 + g->max_reads - 1) / g->max_reads;
+        b.bucket_reads = g->max_reads * ((batches + msw::kLenBuckets - 1) / msw::kLenBuckets);
+    }
+    GZ_TRY(msw::launch_parse_b(b, nlines, any_high, s));
+    GZ_TRY(hipMemcpyAsync(g->h_out, g->d_out, sizeof(msw::ParseOut), hipMemcpyDeviceToHost, s));
+    GZ_TRY(hipEventRecord(g->parsed, s));
+    GZ_TRY(hipStreamSynchronize(s));
     const msw::ParseOut& o = *g->h_out;
     if (trace)
-        fprintf(stderr, "[gfastq] %s span: %zu members%s, %.1f MB in, %.1f MB out: read+index %.2f ms "
+        fprintf(stderr, "[gfastq] %s span: %zu members, %.1f MB in, %.1f MB out: read+index %.2f ms "
                         "(read-ahead join %.2f, window pin %.2f, index %.2f), "
                         "inflate+parse A %.2f ms, parse B %.2f ms (unpin + read-ahead start %.2f), %llu reads\n",
-                g->path.c_str(), g->mem.size(), split ? " (two groups)" : "", used / 1e6, obytes / 1e6, t_read - t0,
-                t_join - t0, t_reg - t_join, t_read - t_reg, t_a - t_read, now_ms() - t_a, t_unpin - t_a,
-                (unsigned long long)o.reads);
+                g->path.c_str(), g->mem.size(), used / 1e6, obytes / 1e6, t_read - t0, t_join - t0, t_reg - t_join,
+                t_read - t_reg, t_a - t_read, now_ms() - t_a, t_unpin - t_a, (unsigned long long)o.reads);
+    if (o.err_over)
+        return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
+                         (unsigned long long)o.err_line);
+    if (o.too_long)
+        return set_error(MSW_E_RANGE, "sequence longer than the slab stride %u at line %llu", g->stride,
+                         (unsigned long long)o.too_long_line);
     g->bytes_in += used;
-    g->bytes_out += o1;
+    g->bytes_out += obytes;
+    g->cur = nx;
+    g->last_buf = nx;
+    g->cur_off = base;
+    g->cur_len = b.len;
+    g->tail_start = o.tail_start;
+    g->started = true;
+    g->at_eof = last;
+    g->span_reads = o.reads;
+    g->span_done = 0;
     ++g->spans;
-    g->part2 = split;
-    g->g2_first = m1;
-    g->g1_out = o1;
-    g->span_obytes = obytes;
-    g->span_used = used;
-    g->span_last = last;
-    return adopt_part(g, nx, slot, last && !split);
+    g->span_min = o.min_len;
+    g->span_max = o.max_len;
+    g->bucket_reads = b.bucket_reads;
+    memcpy(g->span_bmax, o.bmax, sizeof(g->span_bmax));
+    g->sp.v0 = o.v0;
+    g->sp.pending_in = o.pending_in;
+    g->sp.any_high = o.any_high;
+    g->lines += o.valid;
+    g->errors += o.lines - o.valid;
+    g->reads += o.reads;
+    g->bases += o.bases;
+    return MSW_OK;
 }
 
 // Point the reader at a (new) lane file: per-file state back to the start,
@@ -930,7 +791,6 @@ int open_file(msw_gfastq* g, const char* path) {
     g->last_used = 0;
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
     g->pre_indexed = false;
-    g->part2 = false;  // a split span of the last file not read to its end: dropped
     if (g->pf.ok && g->pf.path == path) {
         // prefetched (msw_gfastq_prefetch): file open, mapped, first window
         // [0, reg_len) pinned -- the state register_window leaves behind
@@ -1074,9 +934,7 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     if ((!g->rs && hipStreamCreateWithFlags(&g->rs, hipStreamDefault) != hipSuccess) ||
         hipEventCreateWithFlags(&g->parsed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&g->emitted[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&g->emitted[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&g->lines_emitted[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&g->lines_emitted[1], hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&g->emitted[1], hipEventDisableTiming) != hipSuccess)
         return bail(set_error(MSW_E_DEVICE, "stream/event creation failed"));
     // compressed staging: half a span (FASTQ compresses ~3-4x; less
     // compressible data just makes shorter spans) + room for one fread piece
@@ -1207,12 +1065,10 @@ int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {
     const int k = g->slot;
     g->slot ^= 1;
     GZ_TRY(hipStreamWaitEvent(cs, g->parsed, 0));
-    GZ_TRY(msw::launch_emit_reads(g->pb[g->cur_pb], g->sp, g->span_done, n, g->s_reads[k], g->s_rlen[k],
+    GZ_TRY(msw::launch_emit_reads(g->pb[g->cur], g->sp, g->span_done, n, g->s_reads[k], g->s_rlen[k],
                                   g->want_pos ? g->s_pos[k] : nullptr, cs));
     GZ_TRY(hipEventRecord(g->emitted[g->cur], cs));
     g->emitted_valid[g->cur] = true;
-    GZ_TRY(hipEventRecord(g->lines_emitted[g->cur_pb], cs));
-    g->lines_emitted_valid[g->cur_pb] = true;
     out->reads = g->s_reads[k];
     out->read_len = g->s_rlen[k];
     out->pos = g->want_pos ? g->s_pos[k] : nullptr;

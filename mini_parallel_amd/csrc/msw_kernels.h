@@ -175,6 +175,19 @@ hipError_t launch_cut_windows_for_reads(const uint8_t* genome, uint64_t glen, co
 // bytes from device memory to pinned host memory (dst: its device address),
 // as a kernel on `stream` (msw_memcpy_d2h_async)
 hipError_t launch_d2h_copy(void* dst, const void* src, uint64_t bytes, hipStream_t stream);
+// Up to kPullRanges ranges copied by ONE kernel on `stream`: a one-chunk
+// host call pulls its pinned rows and metadata into the slot's device
+// buffers on its compute stream (no DMA engine, no cross-queue event between
+// the upload and the scoring launch).  Sources are device addresses of
+// pinned host memory; each range's source and destination share their
+// alignment mod 16 (16-byte loads between a byte head and tail).
+constexpr int kPullRanges = 3;
+struct PullRanges {
+    uint8_t* dst[kPullRanges];
+    const uint8_t* src[kPullRanges];
+    uint64_t bytes[kPullRanges];  // 0: unused
+};
+hipError_t launch_pull_copy(const PullRanges& r, hipStream_t stream);
 hipError_t launch_gather_results(const uint32_t* inv, const int32_t* src_score, const int16_t* src_i,
                                  const int16_t* src_j, int32_t* score, int16_t* end_i, int16_t* end_j, uint64_t n,
                                  hipStream_t stream);

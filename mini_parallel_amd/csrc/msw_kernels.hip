@@ -125,6 +125,28 @@ __global__ __launch_bounds__(256) void d2h_copy_kernel(uint8_t* __restrict__ dst
     }
 }
 
+// The ranges of a one-chunk host call, host memory -> HBM (launch_pull_copy):
+// 16-byte loads over PCIe, grid-stride per range.
+__global__ __launch_bounds__(256) void pull_copy_kernel(PullRanges r) {
+    const uint64_t tid = (uint64_t)blockIdx.x * 256u + threadIdx.x, nth = (uint64_t)gridDim.x * 256u;
+#pragma unroll
+    for (int k = 0; k < kPullRanges; ++k) {
+        uint8_t* d = r.dst[k];
+        const uint8_t* s = r.src[k];
+        const uint64_t bytes = r.bytes[k];
+        const uint64_t head = std::min<uint64_t>(bytes, (16u - ((uintptr_t)d & 15u)) & 15u);
+        const uint64_t body = (bytes - head) >> 4;
+        uint4* d4 = reinterpret_cast<uint4*>(d + head);
+        const uint4* s4 = reinterpret_cast<const uint4*>(s + head);
+        for (uint64_t i = tid; i < body; i += nth) d4[i] = s4[i];
+        const uint64_t tail0 = head + 16u * body, rest = head + (bytes - tail0);
+        for (uint64_t i = tid; i < rest; i += nth) {
+            const uint64_t b = i < head ? i : tail0 + (i - head);
+            d[b] = s[b];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Dispatch.
 // ---------------------------------------------------------------------------
@@ -245,6 +267,17 @@ hipError_t launch_d2h_copy(void* dst, const void* src, uint64_t bytes, hipStream
     const uint64_t blocks = std::min<uint64_t>(1024, std::max<uint64_t>(1, (work + 255) / 256));
     hipLaunchKernelGGL(d2h_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (uint8_t*)dst, (const uint8_t*)src,
                        bytes, head, body16);
+    return hipGetLastError();
+}
+
+hipError_t launch_pull_copy(const PullRanges& r, hipStream_t stream) {
+    uint64_t most = 0;
+    for (int k = 0; k < kPullRanges; ++k) most = std::max(most, r.bytes[k] >> 4);
+    // ~4 loads in flight per thread of the largest range, at most 512 blocks
+    // (the PCIe link, not the CUs, bounds it; the call's scoring kernel and
+    // the other stream's share the CUs)
+    const uint64_t blocks = std::min<uint64_t>(512, std::max<uint64_t>(1, (most + 1023) / 1024));
+    hipLaunchKernelGGL(pull_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, r);
     return hipGetLastError();
 }
 

@@ -270,6 +270,8 @@ struct Slot {
     size_t cap_pairs = 0, cap_read = 0, cap_win = 0;
     uint8_t *d_reads = nullptr, *d_wins = nullptr, *d_meta = nullptr, *d_res = nullptr;
     uint8_t *h_reads = nullptr, *h_wins = nullptr, *h_meta = nullptr, *h_res = nullptr;
+    // device addresses of the pinned staging blocks (one-chunk calls pull from them)
+    const uint8_t *g_reads = nullptr, *g_wins = nullptr, *g_meta = nullptr;
     // views into d_meta / h_meta and d_res / h_res
     int64_t *d_pos = nullptr, *h_pos = nullptr;
     uint32_t *d_order = nullptr, *h_order = nullptr;
@@ -327,10 +329,11 @@ struct msw_ctx {
     int device = 0;
     int cu_count = 256;
     Options opt;  // the environment's switches, read at creation
-    // compute: created with the context; the others on first use
-    // (aux_streams): a stream costs 3-30 ms to create (the first few each make
-    // a hardware queue) and as much to destroy, and the --full-wgs workers
-    // and device-resident callers never use them (profiles/r06/c3f/)
+    // compute: created with the context; the others too, unless the context
+    // is lean (MSW_CTX_LEAN: made by the first call that uses them,
+    // aux_streams): a stream costs 3-30 ms to create (the first few each make
+    // a hardware queue) and as much to destroy, and the --full-wgs GPU-reader
+    // workers never use them (profiles/r06/c3f/)
     hipStream_t compute = nullptr, copy = nullptr, d2h = nullptr;
     // multi-chunk calls alternate their chunks' kernels over compute and
     // compute2, so chunk k+1's waves start under chunk k's tail (one stream
@@ -358,6 +361,7 @@ struct msw_ctx {
         const void* p = nullptr;
         size_t bytes = 0;
         bool pinned = false;
+        const uint8_t* dev = nullptr;  // its device address (pinned ranges)
     };
     static constexpr unsigned kPinnedRanges = 16;
     PinnedRange pinned_ranges[kPinnedRanges];
@@ -510,6 +514,14 @@ int grow_host(T** p, size_t n, unsigned flags = hipHostMallocDefault) {
     return MSW_OK;
 }
 
+// The device address of a pinned host block (the pull copy reads it there).
+int dev_addr(const uint8_t* h, const uint8_t** out) {
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, (void*)h, 0));
+    *out = (const uint8_t*)d;
+    return MSW_OK;
+}
+
 int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
     int rc;
     if (!s.uploaded) {
@@ -525,16 +537,21 @@ int ensure_slot(Slot& s, size_t pairs, size_t read_bytes, size_t win_bytes) {
         if ((rc = grow_dev(&s.d_meta, pairs * kMetaBytesPerPair)) ||
             (rc = grow_host(&s.h_meta, pairs * kMetaBytesPerPair)) ||
             (rc = grow_dev(&s.d_res, pairs * kResBytesPerPair)) ||
-            (rc = grow_host(&s.h_res, pairs * kResBytesPerPair, hipHostMallocMapped | hipHostMallocCoherent)))
+            (rc = grow_host(&s.h_res, pairs * kResBytesPerPair, hipHostMallocMapped | hipHostMallocCoherent)) ||
+            (rc = dev_addr(s.h_meta, &s.g_meta)))
             return rc;
         s.cap_pairs = pairs;
     }
     if (read_bytes > s.cap_read) {
-        if ((rc = grow_dev(&s.d_reads, read_bytes)) || (rc = grow_host(&s.h_reads, read_bytes))) return rc;
+        if ((rc = grow_dev(&s.d_reads, read_bytes)) || (rc = grow_host(&s.h_reads, read_bytes)) ||
+            (rc = dev_addr(s.h_reads, &s.g_reads)))
+            return rc;
         s.cap_read = read_bytes;
     }
     if (win_bytes > s.cap_win) {
-        if ((rc = grow_dev(&s.d_wins, win_bytes)) || (rc = grow_host(&s.h_wins, win_bytes))) return rc;
+        if ((rc = grow_dev(&s.d_wins, win_bytes)) || (rc = grow_host(&s.h_wins, win_bytes)) ||
+            (rc = dev_addr(s.h_wins, &s.g_wins)))
+            return rc;
         s.cap_win = win_bytes;
     }
     return MSW_OK;
@@ -1021,7 +1038,9 @@ struct HostBatch {
 
 // True when [p, p + bytes) lies in page-locked host memory (hipHostMalloc /
 // hipHostRegister): such arrays are DMA'd directly, without staging.
-bool is_pinned(const void* p, size_t bytes) {
+// dev: the device address of p when pinned.
+bool is_pinned(const void* p, size_t bytes, const uint8_t** dev) {
+    *dev = nullptr;
     if (!p || !bytes) return false;
     for (const void* q : {p, (const void*)((const uint8_t*)p + bytes - 1)}) {
         hipPointerAttribute_t a;
@@ -1031,6 +1050,7 @@ bool is_pinned(const void* p, size_t bytes) {
             return false;
         }
         if (a.type != hipMemoryTypeHost) return false;
+        if (q == p) *dev = (const uint8_t*)a.devicePointer;
     }
     return true;
 }
@@ -1150,7 +1170,7 @@ bool single_key(const ChunkScan& c, bool all_long) {
 // for the block, which an unpinned one no longer has).
 std::atomic<uint64_t> g_host_free_epoch{0};
 
-bool pinned_cached(msw_ctx* ctx, const void* p, size_t bytes) {
+bool pinned_cached(msw_ctx* ctx, const void* p, size_t bytes, const uint8_t** dev = nullptr) {
     const uint64_t ep = g_host_free_epoch.load(std::memory_order_acquire);
     if (ep != ctx->pinned_epoch) {
         ctx->pinned_used = 0;
@@ -1163,14 +1183,17 @@ bool pinned_cached(msw_ctx* ctx, const void* p, size_t bytes) {
             for (unsigned q = k; q > 0; --q) r[q] = r[q - 1];  // move to front
             r[0] = hit;
             ++ctx->pinned_hits;
+            if (dev) *dev = hit.dev;
             return hit.pinned;
         }
     ++ctx->pinned_misses;
-    const bool pinned = is_pinned(p, bytes);
+    const uint8_t* d = nullptr;
+    const bool pinned = is_pinned(p, bytes, &d);
     const unsigned n = std::min(ctx->pinned_used + 1, msw_ctx::kPinnedRanges);  // the least recent falls off
     for (unsigned q = n - 1; q > 0; --q) r[q] = r[q - 1];
-    r[0] = {p, bytes, pinned};
+    r[0] = {p, bytes, pinned, d};
     ctx->pinned_used = n;
+    if (dev) *dev = d;
     return pinned;
 }
 
@@ -1205,8 +1228,9 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
 
     // Direct DMA from pinned caller arrays; otherwise stage through the slot's
     // pinned buffers with rows repacked to 16-byte-rounded strides.
-    const bool d_reads = pinned_cached(ctx, b.reads, n * b.read_stride);
-    const bool d_wins = !gmode && pinned_cached(ctx, b.wins, n * b.win_stride);
+    const uint8_t *g_reads = nullptr, *g_wins = nullptr;  // their device addresses
+    const bool d_reads = pinned_cached(ctx, b.reads, n * b.read_stride, &g_reads);
+    const bool d_wins = !gmode && pinned_cached(ctx, b.wins, n * b.win_stride, &g_wins);
     const uint32_t rs = d_reads ? b.read_stride : std::min(b.read_stride, std::max(16u, round16(gm)));
     const uint32_t ws = gmode ? std::max(16u, round16(gn))
                               : (d_wins ? b.win_stride : std::min(b.win_stride, std::max(16u, round16(gn))));
@@ -1292,33 +1316,58 @@ int run_batch_impl(msw_ctx* ctx, const msw_scoring_t* sc, const HostBatch& b, ms
         const bool fused = genome_ok && uniform && genome_windows_ok(cnt, cs_.gm, cs_.gn, sch, ctx->cu_count);
         fused_chunks += fused ? 1 : 0;
         if (tr.on) tr.stage += tr.lap();
-        // H2D on the copy stream, kernels on the compute stream (a one-chunk
-        // call: everything on its compute stream).
-        // Async calls upload on the copy stream (an event orders the kernel
-        // after it), so an upload never queues behind its compute stream's
-        // previous kernel.  All on one compute stream, async calls measured
-        // 54-148 us per 10k-pair batch depending on the box (105-148 on two
-        // of three: how the process's streams land on its hardware queues),
-        // with the separate upload 55-57 us on every box
-        // (profiles/r05/host/stream_ab*.jsonl).  A synchronous one-chunk
-        // call keeps the one-stream form (no other call in flight to overlap
-        // with).
-        const bool sep_up = multi_chunk || !sync;
-        hipStream_t up = sep_up ? ctx->copy : cs;
-        HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
-        if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
         // [pos | rlen | wlen | order]: the contiguous part this chunk uses
         const size_t meta_lo = gmode ? 0 : 8 * cnt, meta_hi = (uniform ? 12 : 16) * cnt;
-        HIP_TRY(hipMemcpyAsync(s.d_meta + meta_lo, s.h_meta + meta_lo, meta_hi - meta_lo, hipMemcpyHostToDevice, up));
-        // Pipelined: H2D + window cut on the copy stream, the scoring launch on
-        // the compute stream, results back on the d2h stream -- chunk k+1's
-        // uploads and chunk k-1's readback overlap chunk k's kernel.
-        if (gmode && !fused)
-            HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, b.genome->len, s.d_pos, s.d_wlen, s.d_wins, nullptr, ws,
-                                            cnt, up));
-        if (sep_up) {
-            HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
-            HIP_TRY(hipStreamWaitEvent(cs, s.uploaded, 0));
+        // A one-chunk call pulls its rows and metadata from pinned host
+        // memory into the slot with one copy kernel on its compute stream,
+        // ahead of its scoring launch: no DMA engine and no event between
+        // them.  (The DMA form -- uploads on the copy stream, the kernel
+        // behind an event -- ran the 10k-pair stream at 57 us per batch:
+        // reads and metadata copies 33.6 + 8.0 us back to back on the DMA
+        // engine and ~22 us from an upload's end to its kernel's start,
+        // kernels never overlapping; profiles/r06/host/stream_trace/.)
+        // Sources must share the slot buffers' alignment mod 16.
+        const uint8_t* g_src_reads = d_reads ? g_reads + first * b.read_stride : s.g_reads;
+        const uint8_t* g_src_wins = gmode ? nullptr : (d_wins ? g_wins + first * b.win_stride : s.g_wins);
+        const bool pull = !multi_chunk && g_src_reads && (gmode || g_src_wins) &&
+                          (((uintptr_t)g_src_reads ^ (uintptr_t)s.d_reads) & 15u) == 0 &&
+                          (gmode || (((uintptr_t)g_src_wins ^ (uintptr_t)s.d_wins) & 15u) == 0);
+        if (pull) {
+            msw::PullRanges pr{};
+            pr.dst[0] = s.d_reads;
+            pr.src[0] = g_src_reads;
+            pr.bytes[0] = cnt * rs;
+            if (!gmode) {
+                pr.dst[1] = s.d_wins;
+                pr.src[1] = g_src_wins;
+                pr.bytes[1] = cnt * ws;
+            }
+            pr.dst[2] = s.d_meta + meta_lo;
+            pr.src[2] = s.g_meta + meta_lo;
+            pr.bytes[2] = meta_hi - meta_lo;
+            HIP_TRY(msw::launch_pull_copy(pr, cs));
+            if (gmode && !fused)
+                HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, b.genome->len, s.d_pos, s.d_wlen, s.d_wins, nullptr,
+                                                ws, cnt, cs));
+        } else {
+            // Multi-chunk calls: H2D on the copy stream, kernels on the
+            // compute streams (an event orders each kernel after its chunk's
+            // upload), results back on the d2h stream -- chunk k+1's uploads
+            // and chunk k-1's readback overlap chunk k's kernel.  (One-chunk
+            // calls whose sources are misaligned: DMA'd on the call's own
+            // stream.)
+            hipStream_t up = multi_chunk ? ctx->copy : cs;
+            HIP_TRY(hipMemcpyAsync(s.d_reads, src_reads, cnt * rs, hipMemcpyHostToDevice, up));
+            if (!gmode) HIP_TRY(hipMemcpyAsync(s.d_wins, src_wins, cnt * ws, hipMemcpyHostToDevice, up));
+            HIP_TRY(hipMemcpyAsync(s.d_meta + meta_lo, s.h_meta + meta_lo, meta_hi - meta_lo, hipMemcpyHostToDevice,
+                                   up));
+            if (gmode && !fused)
+                HIP_TRY(msw::launch_cut_windows(b.genome->d_seq, b.genome->len, s.d_pos, s.d_wlen, s.d_wins, nullptr,
+                                                ws, cnt, up));
+            if (multi_chunk) {
+                HIP_TRY(hipEventRecord(s.uploaded, ctx->copy));
+                HIP_TRY(hipStreamWaitEvent(cs, s.uploaded, 0));
+            }
         }
         if (uniform) {
             buckets.resize(1);
@@ -1472,8 +1521,11 @@ int msw_device_info(int ordinal, msw_device_info_t* out) {
     return MSW_OK;
 }
 
-int msw_ctx_create(int ordinal, msw_ctx** out) {
+int msw_ctx_create(int ordinal, msw_ctx** out) { return msw_ctx_create_ex(ordinal, 0u, out); }
+
+int msw_ctx_create_ex(int ordinal, unsigned flags, msw_ctx** out) {
     if (!out) return fail(MSW_E_INVALID, "out is NULL");
+    if (flags & ~MSW_CTX_LEAN) return fail(MSW_E_INVALID, "unknown context flags 0x%x", flags);
     *out = nullptr;
     int n = 0;
     int rc = msw_device_count(&n);
@@ -1487,6 +1539,7 @@ int msw_ctx_create(int ordinal, msw_ctx** out) {
     if (e == hipSuccess && hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->compute, hipStreamNonBlocking);
+    if (e == hipSuccess && !(flags & MSW_CTX_LEAN) && aux_streams(c) != MSW_OK) e = hipErrorOutOfMemory;
     if (e == hipSuccess) e = hipEventCreate(&c->epoch);
     if (e == hipSuccess) e = hipEventRecord(c->epoch, c->compute);
     if (e != hipSuccess) {

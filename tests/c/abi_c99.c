@@ -21,7 +21,7 @@ static int fails = 0;
     } while (0)
 
 int main(int argc, char** argv) {
-    fn_t fns[] = {(fn_t)msw_device_count, (fn_t)msw_device_info, (fn_t)msw_ctx_create,
+    fn_t fns[] = {(fn_t)msw_device_count, (fn_t)msw_device_info, (fn_t)msw_ctx_create, (fn_t)msw_ctx_create_ex,
                    (fn_t)msw_ctx_destroy, (fn_t)msw_align_batch, (fn_t)msw_align_batch_async,
                    (fn_t)msw_wait, (fn_t)msw_align_batch_device, (fn_t)msw_plan_create,
                    (fn_t)msw_align_batch_planned, (fn_t)msw_plan_destroy, (fn_t)msw_align_compat,
@@ -41,6 +41,7 @@ int main(int argc, char** argv) {
     /* NULL arguments are MSW_E_INVALID, never a crash */
     CHECK(msw_device_count(NULL) == MSW_E_INVALID);
     CHECK(msw_ctx_create(0, NULL) == MSW_E_INVALID);
+    CHECK(msw_ctx_create_ex(0, MSW_CTX_LEAN, NULL) == MSW_E_INVALID);
     CHECK(msw_align_batch(NULL, NULL, NULL, NULL, 0) == MSW_E_INVALID);
     CHECK(strlen(msw_last_error()) > 0);
     CHECK(msw_fastq_open("/nonexistent.fastq.gz", NULL) == MSW_E_INVALID);
@@ -63,6 +64,19 @@ int main(int argc, char** argv) {
         CHECK(msw_ctx_create(0, &ctx) == MSW_OK);
         CHECK(msw_align_batch(ctx, &sc, &b, &o, 0) == MSW_OK);
         CHECK(score == 12 && ei == 7 && ej == 6); /* SURVEY.md 8c known answer */
+        msw_ctx_destroy(ctx);
+        /* a lean context: its extra streams made by the first async call */
+        ctx = NULL;
+        score = 0;
+        CHECK(msw_ctx_create_ex(0, 7u, &ctx) == MSW_E_INVALID && ctx == NULL);
+        CHECK(msw_ctx_create_ex(0, MSW_CTX_LEAN, &ctx) == MSW_OK);
+        CHECK(msw_align_batch(ctx, &sc, &b, &o, 0) == MSW_OK && score == 12);
+        {
+            uint64_t t = 0;
+            score = 0;
+            CHECK(msw_align_batch_async(ctx, &sc, &b, &o, 0, &t) == MSW_OK && msw_wait(ctx, t) == MSW_OK);
+            CHECK(score == 12 && ei == 7 && ej == 6);
+        }
         msw_ctx_destroy(ctx);
     }
     if (fails) return 1;

@@ -152,6 +152,7 @@ def test_genome_uniform_chunks(fresh_ctx, oracle, sc, n, chunk, monkeypatch, cap
     mod 16, windows clipped a few bytes short at the genome end, reads with
     N; async calls as bench.py streams them.  MSW_HOST_TRACE shows the path
     (the library reads it when the context is made: fresh_ctx)."""
+    monkeypatch.setenv("MSW_HOST_TRACE", "1")
     rng = np.random.default_rng(n + chunk)
     g = rng.choice(ACGT, 3_000_017)
     pos = rng.integers(0, g.size - 300, n).astype(np.int64)
@@ -166,7 +167,6 @@ def test_genome_uniform_chunks(fresh_ctx, oracle, sc, n, chunk, monkeypatch, cap
     genome = fresh_ctx.load_genome(g)
     W, wl = host_windows(g, pos, want)
     expect = oracle_run(oracle, R, rl, W, wl, sc)
-    monkeypatch.setenv("MSW_HOST_TRACE", "1")
     capfd.readouterr()
     assert_same(fresh_ctx.align_reads(genome, R, rl, pos, want, sc, chunk_pairs=chunk), expect, sc.want_coords)
     trace = [ln for ln in capfd.readouterr().err.splitlines() if ln.startswith("[msw host]")]
@@ -415,3 +415,57 @@ def test_async_stream_upload_forms(gpu_ctx, oracle):
     for p in pend:
         assert_same(p.wait(), expect, sc.want_coords)
     genome.close()
+
+
+@pytest.mark.parametrize("form", ["pairs_pinned", "pairs_pageable", "pairs_misaligned", "genome_pinned"])
+def test_one_chunk_calls_distinct_batches(gpu_ctx, oracle, form):
+    """One-chunk calls pull their rows and metadata from pinned host memory
+    with a copy kernel on their compute stream (no DMA, no event): a stream
+    of async calls over DIFFERENT batches, three in flight, so every staging
+    slot is reused with new data every third call -- pinned arrays read in
+    place, pageable ones staged, pinned rows at an odd address (the DMA form
+    on the call's stream), and reads against a genome.  Every batch must
+    equal the oracle (a stale line of an earlier batch would not)."""
+    sc = SCHEMES[1]
+    batches = [make_pairs(1500 + 7 * k, (120, 160), 2.0, seed=400 + k, read_stride=160, win_stride=336)
+               for k in range(7)]
+
+    def pinned(a, shift=0):
+        buf = pinned_empty(a.nbytes + shift, np.uint8)
+        v = buf[shift:shift + a.nbytes].view(a.dtype).reshape(a.shape)
+        v[...] = a
+        return v
+    genome = None
+    if form == "genome_pinned":
+        rng = np.random.default_rng(9)
+        g = rng.choice(ACGT, 2_000_000)
+        genome = gpu_ctx.load_genome(g)
+    calls = []
+    for k, b in enumerate(batches):
+        if form == "genome_pinned":
+            rng = np.random.default_rng(k)
+            pos = rng.integers(0, 2_000_000 - 400, b.n_pairs).astype(np.int64)
+            want = (2 * b.read_len).astype(np.uint16)
+            W, wl = host_windows(g, pos, want)
+            expect = oracle_run(oracle, b.reads, b.read_len, W, wl, sc)
+            args = (pinned(b.reads), pinned(b.read_len), pinned(pos), pinned(want))
+            calls.append((lambda a=args: gpu_ctx.align_reads(genome, *a, scoring=sc, asynchronous=True), expect))
+        else:
+            expect = oracle_run(oracle, b.reads, b.read_len, b.wins, b.win_len, sc)
+            if form == "pairs_pageable":
+                args = (b.reads, b.read_len, b.wins, b.win_len)
+            else:
+                sh = 1 if form == "pairs_misaligned" else 0
+                args = (pinned(b.reads, sh), pinned(b.read_len), pinned(b.wins, sh), pinned(b.win_len))
+            calls.append((lambda a=args: gpu_ctx.align_batch(*a, sc, asynchronous=True), expect))
+    pend = []
+    for rnd in range(2):  # the same batches again: slots hold other batches' data by then
+        for fn, expect in calls:
+            pend.append((fn(), expect))
+            if len(pend) == 3:
+                p, e = pend.pop(0)
+                assert_same(p.wait(), e, True)
+    for p, e in pend:
+        assert_same(p.wait(), e, True)
+    if genome is not None:
+        genome.close()

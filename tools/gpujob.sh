@@ -18,6 +18,12 @@
 #                          tools/inflate_bench.py at 16384 members (fastq, binned, level 6), MSW_GZ_TIMING kernel times
 #   traffic                tools/traffic_split.sh (FETCH_SIZE of the probe builds, configs 2 and 5)
 #   hostfeed               tools/host_feed.sh (config-4 host feed: copy rates, CLI runs with setup traced)
+#   c3fab=SETTINGS         tools/c3f_env_ab.py, SETTINGS = ';'-separated NAME=VAR=VAL,... (CLI=path: another
+#                          build), 4 alternating rounds, 1 s idle between runs -> c3f_ab.jsonl
+#   c3ftrace[=CLI]         tools/c3f_kernel_trace.sh (kernel trace of config 3 from FASTQ; CLI: another build)
+#   c4ab=CLI               tools/c4_env_ab.py, the in-tree CLI against another build, 2 rounds -> c4_ab.jsonl
+#   stream                 tools/stream_probe.py + tools/wait_probe.py (10k-pair host-to-host stream), and the
+#                          same probe under a kernel + memory-copy trace (stream_trace/)
 # Example: gpurun --timeout 1200 -- bash tools/gpujob.sh r03a tests smoke bench prof
 set -euo pipefail
 T=${1:?tag}
@@ -84,6 +90,24 @@ for step in "$@"; do
       bash tools/traffic_split.sh "$T/traffic" ;;
     hostfeed)
       bash tools/host_feed.sh "$T/hostfeed" ;;
+    c3fab)
+      sets=()
+      IFS=';' read -ra parts <<< "$arg"
+      for p in "${parts[@]}"; do sets+=(--setting "$p"); done
+      timeout -k 10 400 python3 -u tools/c3f_env_ab.py --out "$OUT/c3f_ab.jsonl" "${sets[@]}" --reps 4 --sleep 1 \
+        > "$OUT/c3f_ab.log" 2>&1
+      echo "c3fab ok" ;;
+    c3ftrace)
+      bash tools/c3f_kernel_trace.sh "$T/trace_${arg//\//_}" "--kernel-trace --stats" "${arg:-mini_parallel_amd/rustseq_mini}" ;;
+    c4ab)
+      timeout -k 10 900 python3 -u tools/c4_env_ab.py --cli-b "$arg" --reps 2 --out "$OUT/c4_ab.jsonl" > "$OUT/c4_ab.log" 2>&1
+      echo "c4ab ok" ;;
+    stream)
+      timeout -k 10 120 python3 -u tools/stream_probe.py > "$OUT/stream_probe.jsonl" 2> "$OUT/stream_probe.err"
+      timeout -k 10 120 python3 -u tools/wait_probe.py > "$OUT/wait_probe.json" 2> "$OUT/wait_probe.err"
+      timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/stream_trace" -o st \
+        -- python3 -u tools/stream_probe.py --batches 200 > "$OUT/stream_traced.jsonl" 2> "$OUT/stream_traced.err"
+      cat "$OUT/stream_probe.jsonl" ;;
     *)
       echo "unknown step $name" >&2; exit 2 ;;
   esac

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--trace", action="store_true")
     ap.add_argument("--batches", type=int, default=400)
     ap.add_argument("--pairs", type=int, default=10_000)
+    ap.add_argument("--depths", default="1,2,3,3", help="batches in flight, one pass per entry")
     a = ap.parse_args()
     err_fd = None
     if a.trace:
@@ -50,7 +51,7 @@ def main():
     sc = Scoring()
     want = ctx.align_reads(genome, *arrs, scoring=sc)[0]
     rows = []
-    for depth in (1, 2, 3, 3):
+    for depth in [int(x) for x in a.depths.split(",")]:
         for timed in (False, True):
             n = a.batches if timed else max(50, a.batches // 4)
             pend, sub, wt = [], 0.0, 0.0
