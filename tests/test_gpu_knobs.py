@@ -43,13 +43,16 @@ def _run_cli(tmp_path, ds, extra_env, tag):
 
 @pytest.mark.gpu
 def test_gpu_reader_traces(tmp_path, oracle):
-    """MSW_GFASTQ_TRACE (per-span phase times) and MSW_GZ_TIMING (inflate /
-    CRC kernel times) print their lines; the sums stay the oracle's."""
+    """MSW_GFASTQ_TRACE (per-span phase times), MSW_GZ_TIMING (inflate /
+    CRC kernel times) and MSW_CLI_TRACE (the CLI's per-batch arrival, submit
+    and settle times) print their lines; the sums stay the oracle's."""
     ds, want = _wgs(tmp_path, oracle)
-    rec, err = _run_cli(tmp_path, ds, {"MSW_GPU_INFLATE": "1", "MSW_GFASTQ_TRACE": "1", "MSW_GZ_TIMING": "1"}, "tr")
+    rec, err = _run_cli(tmp_path, ds, {"MSW_GPU_INFLATE": "1", "MSW_GFASTQ_TRACE": "1", "MSW_GZ_TIMING": "1",
+                                       "MSW_CLI_TRACE": "1"}, "tr")
     assert rec["gpu_inflate"] is True and rec["total_score"] == want
     assert "[gfastq]" in err and "span:" in err
     assert "[gz]" in err and "inflate" in err and "crc" in err
+    assert "[cli trace] worker" in err and "submitted" in err and "settled" in err
 
 
 @pytest.mark.gpu
