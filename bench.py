@@ -1478,12 +1478,12 @@ def main(argv=None):
     # reductions and barriers of every leg run through RCCL ("nccl") on the
     # GPUs whatever the GPU count (gloo for --cpu-standin and --share-gpu).
     pg_init = "env://" if "WORLD_SIZE" in os.environ else f"tcp://127.0.0.1:{_free_port()}"
-    dist.init_process_group("nccl" if gpu and not shared else "gloo", init_method=pg_init, rank=rank,
-                            world_size=world, timeout=datetime.timedelta(minutes=30))
     # Build the communicator now, not inside a leg, and keep RCCL's version
-    # banner (printed on stdout at communicator creation) off the one-line
-    # stdout contract.
+    # banner and gloo's connection lines (printed on stdout at communicator
+    # creation) off the one-line stdout contract.
     with _stdout_to_stderr():
+        dist.init_process_group("nccl" if gpu and not shared else "gloo", init_method=pg_init, rank=rank,
+                                world_size=world, timeout=datetime.timedelta(minutes=30))
         from mini_parallel_amd import dist as _md
         _md.sum_over_ranks([0], device=torch.device("cuda", dev_index) if gpu and not shared else None)
     from mini_parallel_amd import dist as mdist
