@@ -761,9 +761,18 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                             const int32_t src = (int32_t)lane - __mul24((int32_t)(q + 1u), (int32_t)d);
                             const bool dep = !lit && src >= 0;
                             const bool far = !lit && src < -(int32_t)RING;
-                            uint32_t val = lit ? (((ti >> 6) >> (8u * (off & 3u))) & 0xFFu)
-                                               : (uint32_t)ring[(opos + (uint32_t)src) & kRingMask];
-                            if (__builtin_amdgcn_ballot_w64(far && lane < W)) {
+                            // Both candidate bytes, then a select: the ring read
+                            // runs on every lane (a literal lane's address is any
+                            // ring byte) instead of behind an exec-mask branch.
+                            uint32_t rbyte = ring[(opos + (uint32_t)src) & kRingMask];
+                            // keeps the load out of a select-to-branch rewrite
+                            asm volatile("" : "+v"(rbyte));
+                            uint32_t val = lit ? (((ti >> 6) >> (8u * (off & 3u))) & 0xFFu) : rbyte;
+                            // Lane masks straight from v_cmp into SGPRs (a ballot of
+                            // a bool went through a VGPR and back: 2 VALU each)
+                            const uint64_t in_w = __builtin_amdgcn_uicmp(lane, W, 36 /* ult */);
+                            const uint64_t not_lit = __builtin_amdgcn_uicmp(ti & 0x40000000u, 0u, 33 /* ne */);
+                            if (__builtin_amdgcn_sicmp(src, -(int32_t)RING, 40 /* slt */) & not_lit & in_w) {
 #if MSW_GZ_PROFILE
                                 const uint64_t t_far = __builtin_amdgcn_s_memtime();
 #endif
@@ -780,7 +789,7 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                             // bytes made by an earlier lane of this window: follow
                             // the pointers (a resolved lane points to itself)
                             uint32_t ptr = dep ? (uint32_t)src : lane;
-                            while (__builtin_amdgcn_ballot_w64(ptr != lane && lane < W)) {
+                            while (__builtin_amdgcn_uicmp(ptr, lane, 33 /* ne */) & in_w) {
                                 const int pa = (int)(ptr << 2);
                                 const uint32_t tv = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)val);
                                 const uint32_t tp = (uint32_t)__builtin_amdgcn_ds_bpermute(pa, (int)ptr);
@@ -788,7 +797,8 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                                 val = settle ? tv : val;
                                 ptr = settle ? lane : tp;
                             }
-                            if (lane < W) ring[(opos + lane) & kRingMask] = (uint8_t)val;
+                            // lanes past the window's W bytes store to their dummy byte
+                            ring[lane < W ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)val;
                             GZP(5, 1);
                             opos += W;
                             if (__builtin_expect(opos - flushed >= kChunk, 0)) {
