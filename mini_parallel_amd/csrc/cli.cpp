@@ -989,8 +989,10 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                                                a.window > 0 ? (uint32_t)a.window : 0u, d.max_len, &o, r.d_wlen,
                                                nullptr) != MSW_OK ||
                         msw_memcpy_d2h_async(ctx.h, r.h, r.d_score, d.n * 4, nullptr) != MSW_OK ||
-                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 4, r.d_ei, d.n * 2, nullptr) != MSW_OK ||
-                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 6, r.d_ej, d.n * 2, nullptr) != MSW_OK ||
+                        // end cells only feed --scores-out records
+                        (sc.want_coords &&
+                         (msw_memcpy_d2h_async(ctx.h, r.h + batch * 4, r.d_ei, d.n * 2, nullptr) != MSW_OK ||
+                          msw_memcpy_d2h_async(ctx.h, r.h + batch * 6, r.d_ej, d.n * 2, nullptr) != MSW_OK)) ||
                         msw_memcpy_d2h_async(ctx.h, r.h + batch * 8, d.read_len, d.n * 2, nullptr) != MSW_OK ||
                         msw_memcpy_d2h_async(ctx.h, r.h + batch * 10, r.d_wlen, d.n * 2, nullptr) != MSW_OK ||
                         msw_fence_record(ctx.h, nullptr, &r.fence) != MSW_OK) {

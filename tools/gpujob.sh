@@ -22,6 +22,7 @@
 #                          build), 4 alternating rounds, 1 s idle between runs -> c3f_ab.jsonl
 #   c3ftrace[=CLI]         tools/c3f_kernel_trace.sh (kernel trace of config 3 from FASTQ; CLI: another build)
 #   c4ab=CLI               tools/c4_env_ab.py, the in-tree CLI against another build, 2 rounds -> c4_ab.jsonl
+#   c4trace                tools/c4_kernel_trace.sh (kernel trace of config 4 at full size, GPU time per kernel family)
 #   stream                 tools/stream_probe.py + tools/wait_probe.py (10k-pair host-to-host stream), and the
 #                          same probe under a kernel + memory-copy trace (stream_trace/)
 # Example: gpurun --timeout 1200 -- bash tools/gpujob.sh r03a tests smoke bench prof
@@ -102,6 +103,8 @@ for step in "$@"; do
     c4ab)
       timeout -k 10 900 python3 -u tools/c4_env_ab.py --cli-b "$arg" --reps 2 --out "$OUT/c4_ab.jsonl" > "$OUT/c4_ab.log" 2>&1
       echo "c4ab ok" ;;
+    c4trace)
+      bash tools/c4_kernel_trace.sh "$T" ;;
     stream)
       timeout -k 10 120 python3 -u tools/stream_probe.py > "$OUT/stream_probe.jsonl" 2> "$OUT/stream_probe.err"
       timeout -k 10 120 python3 -u tools/wait_probe.py > "$OUT/wait_probe.json" 2> "$OUT/wait_probe.err"
