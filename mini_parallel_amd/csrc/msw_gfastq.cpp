@@ -21,12 +21,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <exception>
 #include <string>
 #include <thread>
@@ -168,6 +170,8 @@ struct Inflater {
     uint32_t* d_flag = nullptr;             // [0] any error
     msw::GzCrcConsts* d_crc = nullptr;
     uint32_t* h_flag = nullptr;             // pinned
+    msw::GzMember* h_mem = nullptr;         // pinned copy of the member table (an async upload)
+    size_t h_mem_cap = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // MSW_GZ_TIMING
 
     int init() {
@@ -185,6 +189,9 @@ struct Inflater {
         if (d_flag) (void)hipFree(d_flag);
         if (d_crc) (void)hipFree(d_crc);
         if (h_flag) (void)hipHostFree(h_flag);
+        if (h_mem) (void)hipHostFree(h_mem);
+        h_mem = nullptr;
+        h_mem_cap = 0;
         dc = nullptr;
         d_mem = nullptr;
         d_status = nullptr;
@@ -195,14 +202,33 @@ struct Inflater {
     // upload cbytes of compressed data + the member table, inflate into out,
     // check CRCs.  in_place: the device address of h_comp's pinned pages --
     // the kernel then reads the compressed bytes over PCIe as it decodes
-    // instead of waiting for a DMA of the whole span first.
+    // instead of waiting for a DMA of the whole span first.  pre: a device
+    // buffer that already holds h_comp's cbytes (uploaded ahead on s) and
+    // kInPad bytes of room after them.
     int run(const uint8_t* h_comp, size_t cbytes, const std::vector<msw::GzMember>& mem, uint8_t* out,
-            hipStream_t s, const uint8_t* in_place = nullptr) {
+            hipStream_t s, const uint8_t* in_place = nullptr, uint8_t* pre = nullptr) {
         int rc;
         if ((rc = grow(&d_mem, &mem_cap, mem.size()))) return rc;
         if ((rc = grow(&d_status, &status_cap, mem.size()))) return rc;
+        if (mem.size() > h_mem_cap) {
+            // the previous upload from it finished (callers synchronise s after each run)
+            if (h_mem) (void)hipHostFree(h_mem);
+            h_mem = nullptr;
+            h_mem_cap = 0;
+            const size_t want = mem.size() + mem.size() / 4;
+            if (hipHostMalloc((void**)&h_mem, want * sizeof(msw::GzMember), hipHostMallocDefault) != hipSuccess) {
+                h_mem = nullptr;
+                return set_error(MSW_E_NOMEM, "hipHostMalloc failed (GPU inflate member table)");
+            }
+            h_mem_cap = want;
+        }
         const uint8_t* src = in_place;
         size_t src_bytes = cbytes;
+        if (!src && pre) {
+            GZ_TRY(hipMemsetAsync(pre + cbytes, 0, kInPad, s));
+            src = pre;
+            src_bytes = cbytes + kInPad;
+        }
         if (!src) {
             if ((rc = grow(&dc, &dc_cap, cbytes + kInPad))) return rc;
             if (cbytes) GZ_TRY(hipMemcpyAsync(dc, h_comp, cbytes, hipMemcpyHostToDevice, s));
@@ -210,8 +236,10 @@ struct Inflater {
             src = dc;
             src_bytes = cbytes + kInPad;
         }
-        if (!mem.empty())
-            GZ_TRY(hipMemcpyAsync(d_mem, mem.data(), mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
+        if (!mem.empty()) {
+            memcpy(h_mem, mem.data(), mem.size() * sizeof(msw::GzMember));
+            GZ_TRY(hipMemcpyAsync(d_mem, h_mem, mem.size() * sizeof(msw::GzMember), hipMemcpyHostToDevice, s));
+        }
         GZ_TRY(hipMemsetAsync(d_flag, 0, 4, s));
         const uint32_t n = (uint32_t)mem.size();
         static const bool timing = getenv("MSW_GZ_TIMING") != nullptr;  // kernel times to stderr (tools)
@@ -300,9 +328,14 @@ struct msw_gfastq {
     // compressed bytes read but not yet inflated: hc[0, hc_len).  Two ways
     // to get them (msw_fastq.h):
     //  mapped (default): hc points into the file's read-only mapping; the
-    //    window [reg_lo, fread_off) of the page cache is pinned in place
-    //    (hipHostRegister) and DMA'd to the GPU -- no host copy, no pinned
-    //    staging allocation;
+    //    whole mapping is pinned in place once per file (hipHostRegister) and
+    //    each window [reg_lo, fread_off) DMA'd to the GPU from it -- no host
+    //    copy, no pinned staging allocation.  A finished file stays pinned
+    //    and mapped (retired) until the reader closes or its retired files
+    //    pass retire_cap bytes: hipHostUnregister waits for every stream of
+    //    the device and, for a lane file's 2.3 GB, holds the other threads'
+    //    HIP calls ~24 ms (a pin per window, unpinned per span, held each
+    //    worker until the other's scoring drained: DESIGN 5.1);
     //  copied (MSW_GZ_NO_MAP=1, or when mapping / registering fails): preads
     //    into hc_buf, a hipHostMalloc'ed staging buffer allocated on first use.
     uint8_t* hc = nullptr;
@@ -312,7 +345,26 @@ struct msw_gfastq {
     bool mapped = false;
     uint8_t* map = nullptr;            // whole-file mapping (mapped mode)
     uint64_t map_off = 0;              // first byte not yet inflated
-    uint64_t reg_lo = 0, reg_len = 0;  // the registered window
+    uint64_t reg_lo = 0, reg_len = 0;  // the current window of the mapping
+    bool reg_all = false;              // the whole mapping is pinned
+    // finished files' mappings, pinned (reg) or not, oldest first; unpinned
+    // and unmapped on the retire thread once retired_bytes > retire_cap
+    struct Retired {
+        uint8_t* map;
+        size_t len;
+        bool reg;
+    };
+    std::deque<Retired> retired;
+    uint64_t retired_bytes = 0, retire_cap = 0;
+    std::thread retire;
+    // mapped mode: the next span's compressed window [ahead_lo, + ahead_len)
+    // of mapping ahead_map, DMA'd into d_ahead on the reader stream as soon
+    // as the current span is parsed (upload_ahead), so it crosses PCIe while
+    // the current span is scored instead of in front of the next inflate
+    uint8_t* d_ahead = nullptr;
+    size_t d_ahead_cap = 0;
+    const uint8_t* ahead_map = nullptr;
+    uint64_t ahead_lo = 0, ahead_len = 0;
     bool reg_failed = false;
     // msw_gfastq_prefetch: the next lane file opened, mapped and its first
     // window pinned by a host thread while this file's spans run; open_file
@@ -320,9 +372,11 @@ struct msw_gfastq {
     struct Prefetch {
         std::string path;
         FILE* f = nullptr;
-        uint64_t fsize = 0, reg_len = 0;
+        uint64_t fsize = 0, reg_len = 0;  // reg_len: the first window
         uint8_t* map = nullptr;
+        bool reg = false;  // the whole mapping pinned
         bool ok = false;
+        std::atomic<bool> done{false};  // the thread has finished (ok or not)
         // the first span's member index, built on the same thread (the host
         // walk over the window's member headers; its page touches stalled the
         // reader up to ~20 ms beside other threads' pinning)
@@ -397,12 +451,19 @@ void join_prefetch(msw_gfastq* g) {
 void drop_prefetch(msw_gfastq* g) {
     join_prefetch(g);
     msw_gfastq::Prefetch& p = g->pf;
-    if (p.reg_len) (void)hipHostUnregister(p.map);
+    if (p.map && g->ahead_map == p.map) {  // its first window may still be uploading
+        (void)hipSetDevice(g->device);
+        (void)hipStreamSynchronize(g->rs);
+        g->ahead_map = nullptr;
+        g->ahead_len = 0;
+    }
+    if (p.reg) (void)hipHostUnregister(p.map);
     if (p.map) munmap(p.map, (size_t)p.fsize);
     if (p.f) fclose(p.f);
     p.f = nullptr;
     p.map = nullptr;
     p.fsize = p.reg_len = 0;
+    p.reg = false;
     p.ok = false;
     p.indexed = false;
     p.mem.clear();
@@ -411,15 +472,36 @@ void drop_prefetch(msw_gfastq* g) {
 
 void unmap_file(msw_gfastq* g);
 
+void join_retire(msw_gfastq* g) {
+    if (g->retire.joinable()) g->retire.join();
+}
+
+void free_retired(const std::vector<msw_gfastq::Retired>& v, int dev) {
+    for (const msw_gfastq::Retired& r : v) {
+        if (r.reg && hipSetDevice(dev) == hipSuccess) (void)hipHostUnregister(r.map);
+        munmap(r.map, r.len);
+    }
+}
+
+// every retired file unpinned and unmapped (the reader closes)
+void drain_retired(msw_gfastq* g) {
+    join_retire(g);
+    free_retired(std::vector<msw_gfastq::Retired>(g->retired.begin(), g->retired.end()), g->device);
+    g->retired.clear();
+    g->retired_bytes = 0;
+}
+
 void release(msw_gfastq* g) {
     join_filler(g);
     drop_prefetch(g);
     (void)hipSetDevice(g->device);
     if (g->rs) (void)hipStreamSynchronize(g->rs);
     unmap_file(g);
+    drain_retired(g);
     if (g->f) fclose(g->f);
     for (int i = 0; i < 2; ++i) {
         if (g->dout[i]) (void)hipFree(g->dout[i]);
+        if (i == 0 && g->d_ahead) (void)hipFree(g->d_ahead);
         if (g->s_reads[i]) (void)hipFree(g->s_reads[i]);
         if (g->s_rlen[i]) (void)hipFree(g->s_rlen[i]);
         if (g->s_pos[i]) (void)hipFree(g->s_pos[i]);
@@ -498,17 +580,21 @@ int fill_compressed(msw_gfastq* g, size_t want);
 // Start reading ahead ~one span's compressed bytes (the last span's size; a
 // whole staging buffer at the start of a file) in the background; next_span
 // joins before it touches hc.
-// Mapped mode: pin the next window of the mapping, [map_off rounded down to
-// a page, + in_cap), in the background (cached pages register at ~200 GB/s,
-// tools/host_feed.cpp; cold ones are read from disk here).
+// Mapped mode: the next window of the mapping, [map_off rounded down to a
+// page, + in_cap); the first call of a file pins the whole mapping, in the
+// background (cached pages register at ~200 GB/s, tools/host_feed.cpp; cold
+// ones are read from disk here).
 void register_window(msw_gfastq* g) {
     const uint64_t lo = g->map_off & ~(uint64_t)4095;
     const uint64_t hi = std::min<uint64_t>(g->fsize, lo + g->in_cap);
-    if (hipSetDevice(g->device) != hipSuccess ||
-        hipHostRegister(g->map + lo, (size_t)(hi - lo), hipHostRegisterReadOnly) != hipSuccess) {
-        (void)hipGetLastError();
-        g->reg_failed = true;  // next_span falls back to copies
-        return;
+    if (!g->reg_all) {
+        if (hipSetDevice(g->device) != hipSuccess ||
+            hipHostRegister(g->map, (size_t)g->fsize, hipHostRegisterReadOnly) != hipSuccess) {
+            (void)hipGetLastError();
+            g->reg_failed = true;  // next_span falls back to copies
+            return;
+        }
+        g->reg_all = true;
     }
     g->reg_lo = lo;
     g->reg_len = hi - lo;
@@ -551,13 +637,34 @@ int ensure_stage(msw_gfastq* g) {
     return MSW_OK;
 }
 
-// after the stream drained: unpin the window, drop the mapping
+// after the stream drained: retire the file's mapping (see `retired`); the
+// oldest retired files past retire_cap are unpinned and unmapped on a thread
+// of their own, the caller going on with the next file
 void unmap_file(msw_gfastq* g) {
-    if (g->reg_len) (void)hipHostUnregister(g->map + g->reg_lo);
-    if (g->map) munmap(g->map, (size_t)g->fsize);
+    uint8_t* map = g->map;
+    const size_t len = (size_t)g->fsize;
+    const bool reg = g->reg_all;
     g->map = nullptr;
     g->mapped = false;
+    g->reg_all = false;
     g->reg_lo = g->reg_len = 0;
+    if (!map) return;
+    g->retired.push_back({map, len, reg});
+    g->retired_bytes += len;
+    std::vector<msw_gfastq::Retired> out;
+    while (g->retired_bytes > g->retire_cap && !g->retired.empty()) {
+        out.push_back(g->retired.front());
+        g->retired_bytes -= g->retired.front().len;
+        g->retired.pop_front();
+    }
+    if (out.empty()) return;
+    join_retire(g);
+    const int dev = g->device;
+    try {
+        g->retire = std::thread([out, dev]() { free_retired(out, dev); });
+    } catch (const std::exception&) {
+        free_retired(out, dev);
+    }
 }
 
 // A window could not be pinned: the rest of the file goes through copies.
@@ -571,6 +678,43 @@ int to_copied(msw_gfastq* g) {
     g->hc_len = 0;
     g->fread_off = off;
     return fill_compressed(g, g->hc_cap);
+}
+
+// Mapped mode, after a span is parsed: DMA the next span's window -- this
+// file's next window, or after the file's last span the prefetched next
+// file's first window -- into d_ahead on the reader stream (see d_ahead).
+// Anything not ready (a window still pinning, a prefetch still running)
+// is left to next_span's own upload.
+void upload_ahead(msw_gfastq* g) {
+    g->ahead_map = nullptr;
+    g->ahead_len = 0;
+    if (!g->d_ahead) return;
+    const uint8_t* map = nullptr;
+    uint64_t lo = 0, len = 0;
+    if (g->mapped && !g->at_eof) {
+        join_filler(g);
+        if (g->fill_rc || g->reg_failed || !g->reg_all) return;
+        if (!g->reg_len && g->map_off < g->fsize) register_window(g);
+        if (!g->reg_len || g->reg_failed) return;
+        map = g->map;
+        lo = g->reg_lo;
+        len = g->reg_len;
+    } else if (g->at_eof && g->pf.done.load(std::memory_order_acquire)) {
+        join_prefetch(g);  // finished: no wait
+        if (!g->pf.ok || !g->pf.reg) return;
+        map = g->pf.map;
+        len = g->pf.reg_len;
+    } else {
+        return;
+    }
+    if (len + kInPad > g->d_ahead_cap) return;
+    if (hipMemcpyAsync(g->d_ahead, map + lo, len, hipMemcpyHostToDevice, g->rs) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    g->ahead_map = map;
+    g->ahead_lo = lo;
+    g->ahead_len = len;
 }
 
 double now_ms() {
@@ -649,15 +793,20 @@ int next_span(msw_gfastq* g) {
     // 46 MB, two lanes sharing the link) would come first.  Later spans and
     // large ones are uploaded (their DMA overlaps the previous span's work,
     // and PCIe reads at decode time would slow inflate on a saturated link).
+    uint8_t* pre = nullptr;
+    if (g->mapped && g->ahead_map && g->ahead_map == g->map && g->ahead_lo == g->reg_lo &&
+        used + lead <= g->ahead_len)
+        pre = g->d_ahead;
+    g->ahead_map = nullptr;  // used now, or stale
     const uint8_t* in_place = nullptr;
-    if (g->mapped && g->reg_len && g->cur < 0 && used + lead <= g->in_place_max) {
+    if (!pre && g->mapped && g->reg_len && g->cur < 0 && used + lead <= g->in_place_max) {
         void* dp = nullptr;
         if (hipHostGetDevicePointer(&dp, (void*)(g->hc - lead), 0) == hipSuccess && dp)
             in_place = (const uint8_t*)dp;
         else
             (void)hipGetLastError();
     }
-    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s, in_place))) return rc;
+    if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s, in_place, pre))) return rc;
     // 3. the previous span's unfinished line goes right in front
     const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
     if (carry > kCarry)
@@ -692,8 +841,7 @@ int next_span(msw_gfastq* g) {
     if ((rc = g->inf.check(g->mem, g->path.c_str()))) return rc;
     // the upload of hc has completed: drop the consumed bytes and read ahead
     if (g->mapped) {
-        // the window's upload is done: unpin it; the next one registers in the background
-        (void)hipHostUnregister(g->map + g->reg_lo);
+        // the window's upload is done (the mapping stays pinned until the file closes)
         g->reg_len = 0;
         g->map_off += used;
         g->hc_len = 0;
@@ -759,6 +907,7 @@ int next_span(msw_gfastq* g) {
     g->errors += o.lines - o.valid;
     g->reads += o.reads;
     g->bases += o.bases;
+    upload_ahead(g);
     return MSW_OK;
 }
 
@@ -792,13 +941,14 @@ int open_file(msw_gfastq* g, const char* path) {
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
     g->pre_indexed = false;
     if (g->pf.ok && g->pf.path == path) {
-        // prefetched (msw_gfastq_prefetch): file open, mapped, first window
-        // [0, reg_len) pinned -- the state register_window leaves behind
+        // prefetched (msw_gfastq_prefetch): file open, mapped and pinned, the
+        // first window [0, reg_len) -- the state register_window leaves behind
         msw_gfastq::Prefetch& p = g->pf;
         g->f = p.f;
         g->fsize = p.fsize;
         g->map = p.map;
         g->mapped = true;
+        g->reg_all = p.reg;
         g->map_off = g->reg_lo = 0;
         g->reg_len = p.reg_len;
         g->hc = g->map;
@@ -813,6 +963,7 @@ int open_file(msw_gfastq* g, const char* path) {
         p.f = nullptr;
         p.map = nullptr;
         p.fsize = p.reg_len = 0;
+        p.reg = false;
         p.ok = false;
         p.indexed = false;
         p.mem.clear();
@@ -896,6 +1047,11 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
         if (eip) g->in_place_max = strtoull(eip, nullptr, 10) << 20;
         const char* nm = getenv("MSW_GZ_NO_MAP");
         g->no_map = nm && atoi(nm) != 0;
+        // finished files kept pinned: MSW_GZ_RETIRE_MB, default min(32 GiB, RAM / 8)
+        const char* er = getenv("MSW_GZ_RETIRE_MB");
+        const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+        const uint64_t ram = pages > 0 && psz > 0 ? (uint64_t)pages * (uint64_t)psz : (64ull << 30);
+        g->retire_cap = er ? strtoull(er, nullptr, 10) << 20 : std::min<uint64_t>(32ull << 30, ram / 8);
     }
     if (span_bytes == 0) {
         const char* e = getenv("MSW_GFASTQ_SPAN_MB");
@@ -966,6 +1122,17 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
         const size_t lines = (size_t)(g->span / 32) + 1024;
         const size_t members = (size_t)(g->span / 32768) + 1024;  // BGZF members hold <= 64 KiB
         const size_t tiles = (size_t)((kCarry + g->span + 16 + msw::kParseTile - 1) / msw::kParseTile) + 1;
+        if (!g->no_map) {
+            g->d_ahead_cap = g->in_cap + 4096 + kInPad;
+            if (hipMalloc((void**)&g->d_ahead, g->d_ahead_cap) != hipSuccess) {
+                (void)hipGetLastError();
+                g->d_ahead = nullptr;  // no upload ahead: each span uploads in front of its inflate
+                g->d_ahead_cap = 0;
+            }
+        }
+        if (hipHostMalloc((void**)&g->inf.h_mem, members * sizeof(msw::GzMember), hipHostMallocDefault) != hipSuccess)
+            return bail(set_error(MSW_E_NOMEM, "hipHostMalloc failed (GPU lane reader member table)"));
+        g->inf.h_mem_cap = members;
         if ((rc = grow(&g->inf.dc, &g->inf.dc_cap, g->in_cap + 4096 + kInPad)) ||
             (rc = grow(&g->inf.d_mem, &g->inf.mem_cap, members)) ||
             (rc = grow(&g->inf.d_status, &g->inf.status_cap, members)) ||
@@ -1000,12 +1167,17 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
     drop_prefetch(g);
     if (g->no_map) return MSW_OK;  // copied mode: nothing to pin ahead
     g->pf.path = path;
+    g->pf.done.store(false, std::memory_order_relaxed);
     const size_t cap = g->in_cap;
     const uint64_t span = g->span;
     const int device = g->device;
     msw_gfastq::Prefetch* p = &g->pf;
     try {
         p->th = std::thread([p, cap, span, device]() {
+            struct Done {
+                std::atomic<bool>& d;
+                ~Done() { d.store(true, std::memory_order_release); }
+            } done{p->done};
             // any failure leaves ok = false: reset then opens the file the usual way
             p->f = fopen(p->path.c_str(), "rb");
             if (!p->f) return;
@@ -1022,10 +1194,11 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
             (void)madvise(m, (size_t)p->fsize, MADV_SEQUENTIAL);
             const uint64_t hi = std::min<uint64_t>(p->fsize, cap);
             if (hipSetDevice(device) != hipSuccess ||
-                hipHostRegister(p->map, (size_t)hi, hipHostRegisterReadOnly) != hipSuccess) {
+                hipHostRegister(p->map, (size_t)p->fsize, hipHostRegisterReadOnly) != hipSuccess) {
                 (void)hipGetLastError();
                 return;
             }
+            p->reg = true;
             p->reg_len = hi;
             p->ok = true;
             // the first span's members, as next_span would index them for a

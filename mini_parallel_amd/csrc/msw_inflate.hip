@@ -596,9 +596,10 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
             // the last 112 bits of the member -- go to the scalar step below
             // (one token, the exact bit reader and error rules of the loop it
             // replaces), after which the window resumes at its end.
-            //   info bits: [31] simple, [30] match;
-            //   match:   [5:0] bits, [14:6] length, [29:15] distance - 1
-            //   literal: [3:0] bits, [5:4] count (1..3), [29:6] the bytes
+            //   info bits: [31] simple, [30] match, [5:0] 0 (the walk's slot);
+            //   match:   [14:6] length, [29:15] distance - 1
+            //   literal: [29:6] the bytes (1..3)
+            //   nxo: the next token's lane | output length << 8 (255: not simple)
             // Lanes past the match's end repeat its last byte (the same value to
             // the same ring address), so no lane needs a select or a dummy byte.
             auto copy_near = [&](uint32_t len, uint32_t dist) __attribute__((always_inline)) {
@@ -699,8 +700,10 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     const uint32_t len = (e >> 23) + __builtin_amdgcn_ubfe(x, e & 31u, (e >> 16) & 127u);
                     const uint32_t dist = dbase + __builtin_amdgcn_ubfe(z, ed & 31u, (ed >> 16) & 31u);
                     const uint32_t tm = c + ((ed >> 8) & 31u);
-                    const uint32_t lit = 0x80000000u | (e & 15u) | (((e >> 4) & 3u) << 4) | ((e >> 8) << 6);
-                    const uint32_t mat = 0xC0000000u | tm | (len << 6) | ((dist - 1u) << 15);
+                    // bits 5:0 of both records stay 0: the walk puts the token's
+                    // first output byte in the window there
+                    const uint32_t lit = 0x80000000u | ((e >> 8) << 6);
+                    const uint32_t mat = 0xC0000000u | (len << 6) | ((dist - 1u) << 15);
                     const uint32_t m_lit = 0u - (uint32_t)((e & 0x30u) != 0);
                     // a match resolves here if both codes were in the fast tables
                     // and its distance reaches no further back than the output
@@ -727,37 +730,41 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     // lane by pointer jumping -- and one ring write stores the
                     // window's W bytes.  Windows of more than 64 output bytes take
                     // the serial walk.
-                    const uint32_t m_match = 0u - ((info >> 30) & 1u);
-                    const uint32_t olen = (((info >> 6) & 511u) & m_match) | (((info >> 4) & 3u) & ~m_match);
-                    const uint32_t nbits = ((info & 63u) & m_match) | ((info & 15u) & ~m_match);
                     // (a lane whose token is not simple: next lane 255, length 0)
-                    const uint32_t nxo = (int32_t)info < 0 ? (lane + nbits) | (olen << 8) : 255u;
-                    uint32_t W = 0, ti = 0, to = 0;
+                    uint32_t nx_lit = (lane + (e & 15u)) | (((e >> 4) & 3u) << 8), nx_mat = (lane + tm) | (len << 8);
+                    asm volatile("" : "+v"(nx_lit), "+v"(nx_mat));  // both on every lane, then selects
+                    const uint32_t nxo = m_lit ? nx_lit : (m_mat ? nx_mat : 255u);
+                    // The chain's first token starts the window: every lane takes
+                    // it.  A later token's record carries its first byte W in bits
+                    // 5:0 (OR'd on the scalar unit; W < 64 for every token of a
+                    // window that emits), so a lane's select is one v_cndmask.
+                    uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)nxo, 0);
+                    uint32_t ti = (uint32_t)__builtin_amdgcn_readlane((int)info, 0);
+                    uint32_t W = t >> 8;
                     // one exit: k leaves the window (>= 64) or hits a token that
                     // is not simple (255; the token at kp, which added nothing)
                     uint32_t kp = 0;
-                    k = 0;
-                    do {
-                        const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)nxo, (int)k);
-                        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k);
-                        const bool take = lane >= W;
-                        ti = take ? s0 : ti;
-                        to = take ? W : to;
+                    k = t & 255u;
+                    while (k < 64) {
+                        t = (uint32_t)__builtin_amdgcn_readlane((int)nxo, (int)k);
+                        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k) | W;
+                        ti = lane >= W ? s0 : ti;
                         W += t >> 8;
                         kp = k;
                         k = t & 255u;
-                    } while (k < 64);
+                    }
                     if (k == 255u) k = kp;
                     if (W <= 64u) {
                         if (W) {
-                            const uint32_t off = lane - to;
+                            // offset in the token: lane - its first byte (ti's bits 5:0)
+                            const uint32_t off = (lane - ti) & 63u;
                             const bool lit = (ti & 0x40000000u) == 0;
                             const uint32_t d = ((ti >> 15) & 0x7FFFu) + 1u;
                             // overlapping copies repeat the token's last d bytes:
                             // r = off mod d (see rmag; lane address wraps mod 64)
                             const uint32_t m = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(d, 64u) << 2), (int)rmag);
                             const uint32_t q = __umul24(off, m) >> 12;  // floor(off / d)
-                            // window-relative source: to + (off mod d) - d = lane - d (q + 1)
+                            // window-relative source: start + (off mod d) - d = lane - d (q + 1)
                             const int32_t src = (int32_t)lane - __mul24((int32_t)(q + 1u), (int32_t)d);
                             const bool dep = !lit && src >= 0;
                             const bool far = !lit && src < -(int32_t)RING;
@@ -814,18 +821,19 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                         uint32_t kstop = 0;
                         do {
                             const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k);
+                            const uint32_t tn = (uint32_t)__builtin_amdgcn_readlane((int)nxo, (int)k);
                             if (s & 0x40000000u) {
-                                const uint32_t ln = (s >> 6) & 511u, ds = ((s >> 15) & 0x7FFFu) + 1u;
+                                const uint32_t ln = tn >> 8, ds = ((s >> 15) & 0x7FFFu) + 1u;
                                 GZP(5, 1);
                                 copy_match(ln, ds);
                                 opos += ln;
-                                k += s & 63u;
+                                k = tn & 255u;
                             } else if ((int32_t)s < 0) {
                                 GZP(2, 1);
-                                const uint32_t nlit = (s >> 4) & 3u;
+                                const uint32_t nlit = tn >> 8;
                                 ring[lane < nlit ? ((opos + lane) & kRingMask) : dummy] = (uint8_t)(s >> lit_shift6);
                                 opos += nlit;
-                                k += s & 15u;
+                                k = tn & 255u;
                             } else {
                                 kstop = k;  // not a simple token: the scalar step takes it
                                 k = 0x10000u;

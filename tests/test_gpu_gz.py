@@ -225,9 +225,9 @@ def _reader_mode(monkeypatch, mode):
 @pytest.mark.parametrize("block", [0xFF00, 1000])
 @pytest.mark.parametrize("crlf", [False, True])
 def test_reader_matches_host_reader(gpu_ctx, tmp_path, monkeypatch, block, crlf, mode):
-    """mode "map": compressed bytes from the file's mapping (page-cache pages
-    pinned in place, one window per span starting at the page boundary below
-    the span), the file's first span read by the inflate kernel in place over
+    """mode "map": compressed bytes from the file's mapping (its page-cache
+    pages pinned in place once, one window per span starting at the page
+    boundary below the span), the file's first span read by the inflate kernel in place over
     PCIe and later spans DMA'd; "map_upload": every span DMA'd
     (MSW_GZ_IN_PLACE_MB=0); "copy": preads into pinned staging
     (MSW_GZ_NO_MAP=1)."""
@@ -279,13 +279,21 @@ def test_reader_prefetch_next_file(gpu_ctx, tmp_path, monkeypatch, mode):
         assert np.array_equal(hl, gl) and np.array_equal(hp, gp) and np.array_equal(hs, gs), f
 
 
+@pytest.mark.parametrize("retire", [None, "0"])
 @pytest.mark.parametrize("span", [1 << 20, 1 << 18])
-def test_reader_prefetch_chain(gpu_ctx, tmp_path, monkeypatch, span):
+def test_reader_prefetch_chain(gpu_ctx, tmp_path, monkeypatch, span, retire):
     """Lane files read back to back, each with the next one prefetched (the
     --full-wgs worker's order: reset, then prefetch the file after it), so
     every file after the first is adopted with its first span indexed on the
-    prefetch thread; every file reads exactly as the host reader reads it."""
+    prefetch thread; every file reads exactly as the host reader reads it.
+    A finished file stays pinned until the reader closes (default), or, with
+    MSW_GZ_RETIRE_MB=0, is unpinned and unmapped on the retire thread as the
+    next one opens."""
     monkeypatch.setenv("MSW_GZ_NO_MAP", "0")
+    if retire is None:
+        monkeypatch.delenv("MSW_GZ_RETIRE_MB", raising=False)
+    else:
+        monkeypatch.setenv("MSW_GZ_RETIRE_MB", retire)
     files = []
     for k in range(5):
         p = tmp_path / f"lane{k}.fastq.gz"
