@@ -363,6 +363,10 @@ struct msw_gfastq {
     // the current span is scored instead of in front of the next inflate
     uint8_t* d_ahead = nullptr;
     size_t d_ahead_cap = 0;
+    // false from a file's open until its first span is in: the prefetch
+    // thread pins the next file only then (a 2.3 GB pin beside the first
+    // span's upload and inflate stretched that span from ~15 to ~130 ms)
+    std::atomic<bool> first_span_in{true};
     const uint8_t* ahead_map = nullptr;
     uint64_t ahead_lo = 0, ahead_len = 0;
     bool reg_failed = false;
@@ -377,6 +381,7 @@ struct msw_gfastq {
         bool reg = false;  // the whole mapping pinned
         bool ok = false;
         std::atomic<bool> done{false};  // the thread has finished (ok or not)
+        std::atomic<bool> cancel{false};  // drop_prefetch: stop waiting
         // the first span's member index, built on the same thread (the host
         // walk over the window's member headers; its page touches stalled the
         // reader up to ~20 ms beside other threads' pinning)
@@ -449,7 +454,9 @@ void join_prefetch(msw_gfastq* g) {
 }
 
 void drop_prefetch(msw_gfastq* g) {
+    g->pf.cancel.store(true, std::memory_order_release);
     join_prefetch(g);
+    g->pf.cancel.store(false, std::memory_order_relaxed);
     msw_gfastq::Prefetch& p = g->pf;
     if (p.map && g->ahead_map == p.map) {  // its first window may still be uploading
         (void)hipSetDevice(g->device);
@@ -807,6 +814,7 @@ int next_span(msw_gfastq* g) {
             (void)hipGetLastError();
     }
     if ((rc = g->inf.run(g->hc - lead, used + lead, g->mem, g->dout[nx], s, in_place, pre))) return rc;
+    const double t_run = trace ? now_ms() : 0.0;
     // 3. the previous span's unfinished line goes right in front
     const uint64_t carry = g->cur < 0 ? 0 : g->cur_len - g->tail_start;
     if (carry > kCarry)
@@ -875,9 +883,11 @@ int next_span(msw_gfastq* g) {
     if (trace)
         fprintf(stderr, "[gfastq] %s span: %zu members, %.1f MB in, %.1f MB out: read+index %.2f ms "
                         "(read-ahead join %.2f, window pin %.2f, index %.2f), "
-                        "inflate+parse A %.2f ms, parse B %.2f ms (unpin + read-ahead start %.2f), %llu reads\n",
+                        "inflate+parse A %.2f ms (host calls %.2f, %s), parse B %.2f ms (read-ahead start %.2f), "
+                        "%llu reads\n",
                 g->path.c_str(), g->mem.size(), used / 1e6, obytes / 1e6, t_read - t0, t_join - t0, t_reg - t_join,
-                t_read - t_reg, t_a - t_read, now_ms() - t_a, t_unpin - t_a, (unsigned long long)o.reads);
+                t_read - t_reg, t_a - t_read, t_run - t_read, pre ? "uploaded ahead" : (in_place ? "in place" : "upload"),
+                now_ms() - t_a, t_unpin - t_a, (unsigned long long)o.reads);
     if (o.err_over)
         return set_error(MSW_E_INVALID, "Too many read errors (>10), stopping at line %llu",
                          (unsigned long long)o.err_line);
@@ -908,6 +918,7 @@ int next_span(msw_gfastq* g) {
     g->reads += o.reads;
     g->bases += o.bases;
     upload_ahead(g);
+    g->first_span_in.store(true, std::memory_order_release);
     return MSW_OK;
 }
 
@@ -940,6 +951,7 @@ int open_file(msw_gfastq* g, const char* path) {
     g->last_used = 0;
     g->lines = g->reads = g->errors = g->bases = g->bytes_in = g->bytes_out = 0;
     g->pre_indexed = false;
+    g->first_span_in.store(false, std::memory_order_release);
     if (g->pf.ok && g->pf.path == path) {
         // prefetched (msw_gfastq_prefetch): file open, mapped and pinned, the
         // first window [0, reg_len) -- the state register_window leaves behind
@@ -1092,6 +1104,10 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
         hipEventCreateWithFlags(&g->emitted[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&g->emitted[1], hipEventDisableTiming) != hipSuccess)
         return bail(set_error(MSW_E_DEVICE, "stream/event creation failed"));
+    // the reader's kernels' code objects, loaded with the reader instead of
+    // at the first span (two workers' first launches each waited ~80 ms there)
+    if (msw::gz_preload() != hipSuccess || msw::parse_preload() != hipSuccess)
+        return bail(set_error(MSW_E_DEVICE, "GPU lane reader: kernel load failed"));
     // compressed staging: half a span (FASTQ compresses ~3-4x; less
     // compressible data just makes shorter spans) + room for one fread piece
     g->in_cap = (size_t)(std::max<uint64_t>(g->span / 2, 16u << 20) + kReadPiece + (1u << 20));
@@ -1172,8 +1188,9 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
     const uint64_t span = g->span;
     const int device = g->device;
     msw_gfastq::Prefetch* p = &g->pf;
+    std::atomic<bool>* gate = &g->first_span_in;
     try {
-        p->th = std::thread([p, cap, span, device]() {
+        p->th = std::thread([p, cap, span, device, gate]() {
             struct Done {
                 std::atomic<bool>& d;
                 ~Done() { d.store(true, std::memory_order_release); }
@@ -1193,6 +1210,12 @@ int msw_gfastq_prefetch(msw_gfastq* g, const char* path) {
             p->map = (uint8_t*)m;
             (void)madvise(m, (size_t)p->fsize, MADV_SEQUENTIAL);
             const uint64_t hi = std::min<uint64_t>(p->fsize, cap);
+            // pin once the current file's first span is in (bounded wait)
+            for (int i = 0; i < 20000 && !gate->load(std::memory_order_acquire); ++i) {
+                if (p->cancel.load(std::memory_order_acquire)) return;
+                usleep(250);
+            }
+            if (p->cancel.load(std::memory_order_acquire)) return;
             if (hipSetDevice(device) != hipSuccess ||
                 hipHostRegister(p->map, (size_t)p->fsize, hipHostRegisterReadOnly) != hipSuccess) {
                 (void)hipGetLastError();

@@ -56,6 +56,10 @@ hipError_t launch_gz_inflate(const uint8_t* cdata, size_t cbytes, const GzMember
 // CRC-32 of every member's output against its trailer (one wave per member).
 hipError_t launch_gz_crc(const uint8_t* out, const GzMember* members, uint32_t n, const GzCrcConsts* consts,
                          uint32_t* status, uint32_t* any_error, hipStream_t stream);
+// Load the inflate / CRC and the parse / emit code objects now (a reader's
+// setup) instead of at their first launch, which sat inside the first span.
+hipError_t gz_preload();
+hipError_t parse_preload();
 
 // ---------------------------------------------------------------------------
 // FASTQ parse of an inflated span (msw_parse.hip).  The span buffer holds the

@@ -1085,6 +1085,11 @@ hipError_t launch_gz_inflate(const uint8_t* cdata, size_t cbytes, const GzMember
     return hipGetLastError();
 }
 
+hipError_t gz_preload() {
+    int nb = 0;  // an occupancy query loads the kernel's code object (msw_ctx_prepare does the same)
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gz_crc_kernel, 256, 0);
+}
+
 hipError_t launch_gz_crc(const uint8_t* out, const GzMember* members, uint32_t n, const GzCrcConsts* consts,
                          uint32_t* status, uint32_t* any_error, hipStream_t stream) {
     if (n == 0) return hipSuccess;

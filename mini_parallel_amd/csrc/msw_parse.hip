@@ -534,6 +534,11 @@ __global__ __launch_bounds__(256) void k_emit(ParseBufs b, EmitSpan sp, uint64_t
 
 }  // namespace
 
+hipError_t parse_preload() {
+    int nb = 0;  // an occupancy query loads the kernel's code object (msw_ctx_prepare does the same)
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_count, 256, 0);
+}
+
 hipError_t launch_parse_a(const ParseBufs& b, hipStream_t stream) {
     const uint32_t nt = b.ntiles ? b.ntiles : 1;
     hipLaunchKernelGGL(k_count, dim3(nt), dim3(256), 0, stream, b);
