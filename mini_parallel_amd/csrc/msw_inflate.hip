@@ -91,6 +91,15 @@ __device__ __forceinline__ uint32_t sbfe(uint32_t v, uint32_t ctl) {
     return d;
 }
 
+// v_bfe_u32 d, v, off, wid: (v >> off[4:0]) & ((1 << wid[4:0]) - 1) per lane;
+// the hardware reads only those bits, so a fast-table entry is passed whole
+// as off and shifted once as wid (no masks)
+__device__ __forceinline__ uint32_t vbfe(uint32_t v, uint32_t off, uint32_t wid) {
+    uint32_t d;
+    asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(d) : "v"(v), "v"(off), "v"(wid));
+    return d;
+}
+
 __device__ __forceinline__ uint32_t len_base(uint32_t sym, uint32_t& extra) {
     if (sym < 265) { extra = 0; return sym - 254; }
     if (sym < 285) { extra = (sym - 261) >> 2; return ((4u + ((sym - 265) & 3u)) << extra) + 3u; }
@@ -686,7 +695,10 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     // lane L's stream bits from bit P + L: dwords j .. j + 2 of the
                     // window, j = (pb + L) / 32, fetched from `cur` across lanes
                     const uint32_t o = pb + lane, bs = o & 31u;
-                    const int a0 = (int)(((pw - br.wbase) + (o >> 5)) << 2);
+                    const uint32_t base4 = (pw - br.wbase) << 2;  // uniform: scalar unit
+                    uint32_t dw = o >> 5;
+                    asm("" : "+v"(dw));  // keeps (o >> 5) << 2 from becoming a shift and a mask
+                    const int a0 = (int)((dw << 2) + base4);  // one v_lshl_add_u32
                     const uint32_t A = (uint32_t)__builtin_amdgcn_ds_bpermute(a0, (int)br.cur);
                     const uint32_t B = (uint32_t)__builtin_amdgcn_ds_bpermute(a0 + 4, (int)br.cur);
                     const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(a0 + 8, (int)br.cur);
@@ -697,8 +709,9 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     const uint32_t z = __builtin_amdgcn_alignbit(y, x, c);  // the distance's bits
                     const uint32_t di = z & ((1u << kFastDBits) - 1u);
                     const uint32_t ed = S.fast_d[di], dbase = S.fast_dbase[di];
-                    const uint32_t len = (e >> 23) + __builtin_amdgcn_ubfe(x, e & 31u, (e >> 16) & 127u);
-                    const uint32_t dist = dbase + __builtin_amdgcn_ubfe(z, ed & 31u, (ed >> 16) & 31u);
+                    // (entries laid out for bfe: offset in [4:0], width in [20:16]; see kFastMatch)
+                    const uint32_t len = (e >> 23) + vbfe(x, e, e >> 16);
+                    const uint32_t dist = dbase + vbfe(z, ed, ed >> 16);
                     const uint32_t tm = c + ((ed >> 8) & 31u);
                     // bits 5:0 of both records stay 0: the walk puts the token's
                     // first output byte in the window there
