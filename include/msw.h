@@ -245,6 +245,15 @@ int msw_synchronize(msw_ctx* ctx);
  * on once; the context keeps unwaited fences until it is destroyed. */
 int msw_fence_record(msw_ctx* ctx, void* stream, uint64_t* fence);
 int msw_fence_wait(msw_ctx* ctx, uint64_t fence);
+/* A stream of the context's device for callers that keep two batches in
+ * flight (e.g. --full-wgs alternates its batches over the compute stream and
+ * one of these, so one batch's read emit and window cut run beside the other
+ * batch's scoring).  Any call taking `void* stream` accepts it; calls on two
+ * streams may run concurrently.  msw_synchronize drains it; msw_ctx_destroy
+ * destroys any the caller has not.  (The reference scores one batch at a
+ * time on one queue: gpu.rs:117-125.) */
+int msw_stream_create(msw_ctx* ctx, void** out);
+int msw_stream_destroy(msw_ctx* ctx, void* stream);
 
 /* Counters of the host-batch calls (msw_align_batch*, msw_align_reads*) on a
  * context, for run records (the reference's BenchmarkResult,

@@ -30,6 +30,7 @@ EXPORTED = (
     "msw_genome_create", "msw_genome_destroy", "msw_genome_length", "msw_align_reads",
     "msw_align_reads_async", "msw_genome_cut_device", "msw_ctx_stats", "msw_align_reads_device",
     "msw_memcpy_d2h_async", "msw_fence_record", "msw_fence_wait", "msw_ctx_prepare",
+    "msw_stream_create", "msw_stream_destroy",
 )
 # include/msw_fastq.h
 FASTQ_EXPORTED = ("msw_fastq_open", "msw_fastq_close", "msw_fastq_next", "msw_fastq_next_packed",
@@ -132,6 +133,8 @@ def _declare(L):
         "msw_memcpy_d2h_async": (I, [P, P, P, ctypes.c_size_t, P]),
         "msw_fence_record": (I, [P, P, ctypes.POINTER(ctypes.c_uint64)]),
         "msw_fence_wait": (I, [P, ctypes.c_uint64]),
+        "msw_stream_create": (I, [P, ctypes.POINTER(P)]),
+        "msw_stream_destroy": (I, [P, P]),
         "msw_synchronize": (I, [P]),
         "msw_ctx_stats": (I, [P, ctypes.POINTER(StatsT), I]),
         "msw_ctx_prepare": (I, [P, ctypes.POINTER(ScoringT)]),

@@ -792,6 +792,17 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 // lean: a GPU-reader worker scores device-resident batches
                 // only, so its context makes just the compute stream
                 Ctx ctx(devices[gi].ordinal, MSW_CTX_LEAN);
+                // With per-read records (256k-read batches) the batches
+                // alternate over two streams (with the two result sets), so
+                // one batch's read emit and window cut run beside the other
+                // batch's scoring instead of between two launches: config 3
+                // from FASTQ 13.67-13.99 -> 13.25-13.74 ms.  Sums only (1 M-read
+                // batches that fill the GPU alone) keep one stream: config 4
+                // measured 3 % slower on two.
+                void* st2 = nullptr;
+                if (!a.scores_out.empty() && msw_stream_create(ctx.h, &st2) != MSW_OK)
+                    die(std::string("GPU stream: ") + msw_last_error());
+                void* const streams[2] = {nullptr, st2};
                 const double t_ctx = ms_since(ts0);
                 msw_gfastq* gr = nullptr;  // one reader per worker, reset per file (buffers kept)
                 if (msw_gfastq_open(ctx.h, nullptr, read_stride(), batch, 1, 0, &gr) != MSW_OK)
@@ -968,7 +979,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                 while (have) {
                     FileState& f = *st[fi];
                     msw_dev_reads_t d;
-                    if (msw_gfastq_next(gr, nullptr, &d) != MSW_OK) {
+                    void* const bs = streams[cur];  // this batch's stream
+                    if (msw_gfastq_next(gr, bs, &d) != MSW_OK) {
                         f.error = msw_last_error();
                         fprintf(stderr, "  Error reading %s: %s\n", f.path.c_str(), f.error.c_str());
                         f.failed = true;
@@ -987,15 +999,15 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     msw_out_t o{r.d_score, r.d_ei, r.d_ej};
                     if (msw_align_reads_device(ctx.h, &sc, gen, d.reads, d.read_len, d.read_stride, d.pos, d.n,
                                                a.window > 0 ? (uint32_t)a.window : 0u, d.max_len, &o, r.d_wlen,
-                                               nullptr) != MSW_OK ||
-                        msw_memcpy_d2h_async(ctx.h, r.h, r.d_score, d.n * 4, nullptr) != MSW_OK ||
+                                               bs) != MSW_OK ||
+                        msw_memcpy_d2h_async(ctx.h, r.h, r.d_score, d.n * 4, bs) != MSW_OK ||
                         // end cells only feed --scores-out records
                         (sc.want_coords &&
-                         (msw_memcpy_d2h_async(ctx.h, r.h + batch * 4, r.d_ei, d.n * 2, nullptr) != MSW_OK ||
-                          msw_memcpy_d2h_async(ctx.h, r.h + batch * 6, r.d_ej, d.n * 2, nullptr) != MSW_OK)) ||
-                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 8, d.read_len, d.n * 2, nullptr) != MSW_OK ||
-                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 10, r.d_wlen, d.n * 2, nullptr) != MSW_OK ||
-                        msw_fence_record(ctx.h, nullptr, &r.fence) != MSW_OK) {
+                         (msw_memcpy_d2h_async(ctx.h, r.h + batch * 4, r.d_ei, d.n * 2, bs) != MSW_OK ||
+                          msw_memcpy_d2h_async(ctx.h, r.h + batch * 6, r.d_ej, d.n * 2, bs) != MSW_OK)) ||
+                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 8, d.read_len, d.n * 2, bs) != MSW_OK ||
+                        msw_memcpy_d2h_async(ctx.h, r.h + batch * 10, r.d_wlen, d.n * 2, bs) != MSW_OK ||
+                        msw_fence_record(ctx.h, bs, &r.fence) != MSW_OK) {
                         fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
                         f.failed = true;
                         (void)msw_synchronize(ctx.h);

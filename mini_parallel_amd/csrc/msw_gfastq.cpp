@@ -314,8 +314,11 @@ struct msw_gfastq {
     // that read it, on the caller's stream.  A span only waits for the emits
     // of the span two before it, so inflating and parsing the next span (or
     // the next file) runs beside the current span's emits and scoring.
-    hipEvent_t emitted[2] = {nullptr, nullptr};
-    bool emitted_valid[2] = {false, false};
+    // The last two emits of each buffer (a caller may alternate two
+    // streams: each stream's last emit covers its earlier ones).
+    hipEvent_t emitted[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    bool emitted_valid[2][2] = {{false, false}, {false, false}};
+    int emit_slot[2] = {0, 0};
     int last_buf = 1;                  // buffer of the latest span (any file); the next takes the other
     FILE* f = nullptr;
     std::string path;
@@ -529,7 +532,7 @@ void release(msw_gfastq* g) {
     if (g->hc_buf) (void)hipHostFree(g->hc_buf);
     g->inf.release();
     if (g->parsed) (void)hipEventDestroy(g->parsed);
-    for (hipEvent_t e : g->emitted)
+    for (hipEvent_t e : {g->emitted[0][0], g->emitted[0][1], g->emitted[1][0], g->emitted[1][1]})
         if (e) (void)hipEventDestroy(e);
     if (g->rs) (void)hipStreamDestroy(g->rs);
     delete g;
@@ -787,7 +790,8 @@ int next_span(msw_gfastq* g) {
     // dout[nx] and its line arrays were last read by the emits of the span
     // before the current one (long finished, normally); the current span's
     // emits and the caller's scoring keep running
-    if (g->emitted_valid[nx]) GZ_TRY(hipStreamWaitEvent(s, g->emitted[nx], 0));
+    for (int j = 0; j < 2; ++j)
+        if (g->emitted_valid[nx][j]) GZ_TRY(hipStreamWaitEvent(s, g->emitted[nx][j], 0));
     // 2. inflate + CRC into dout[nx] at kCarry (mapped: the upload starts at
     // the page boundary below hc, inside the registered window)
     const size_t lead = g->mapped ? (size_t)(g->map_off - g->reg_lo) : 0;
@@ -1101,8 +1105,10 @@ int msw_gfastq_open(msw_ctx* ctx, const char* path, uint32_t read_stride, uint64
     }
     if ((!g->rs && hipStreamCreateWithFlags(&g->rs, hipStreamDefault) != hipSuccess) ||
         hipEventCreateWithFlags(&g->parsed, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&g->emitted[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&g->emitted[1], hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&g->emitted[0][0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->emitted[0][1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->emitted[1][0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->emitted[1][1], hipEventDisableTiming) != hipSuccess)
         return bail(set_error(MSW_E_DEVICE, "stream/event creation failed"));
     // the reader's kernels' code objects, loaded with the reader instead of
     // at the first span (two workers' first launches each waited ~80 ms there)
@@ -1263,8 +1269,12 @@ int msw_gfastq_next(msw_gfastq* g, void* stream, msw_dev_reads_t* out) {
     GZ_TRY(hipStreamWaitEvent(cs, g->parsed, 0));
     GZ_TRY(msw::launch_emit_reads(g->pb[g->cur], g->sp, g->span_done, n, g->s_reads[k], g->s_rlen[k],
                                   g->want_pos ? g->s_pos[k] : nullptr, cs));
-    GZ_TRY(hipEventRecord(g->emitted[g->cur], cs));
-    g->emitted_valid[g->cur] = true;
+    {
+        const int j = g->emit_slot[g->cur];
+        g->emit_slot[g->cur] ^= 1;
+        GZ_TRY(hipEventRecord(g->emitted[g->cur][j], cs));
+        g->emitted_valid[g->cur][j] = true;
+    }
     out->reads = g->s_reads[k];
     out->read_len = g->s_rlen[k];
     out->pos = g->want_pos ? g->s_pos[k] : nullptr;

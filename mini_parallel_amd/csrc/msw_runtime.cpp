@@ -374,9 +374,18 @@ struct msw_ctx {
     size_t c_cap = 0;
     hipEvent_t c_k0 = nullptr, c_k1 = nullptr;  // timing of the compat launch (msw_ctx_stats)
     // msw_align_reads_device scratch: the cut windows and their clipped lengths
-    uint8_t* r_wins = nullptr;
-    uint16_t* r_wlen = nullptr;
-    size_t r_wins_cap = 0, r_wlen_cap = 0;
+    // msw_align_reads_device's window slab and lengths, one set per stream
+    // it is called on (calls on two streams run concurrently)
+    struct ReadsScratch {
+        hipStream_t st = nullptr;
+        uint8_t* wins = nullptr;
+        uint16_t* wlen = nullptr;
+        size_t wins_cap = 0, wlen_cap = 0;
+    };
+    std::vector<ReadsScratch> rscratch;
+    // streams made by msw_stream_create (synchronised by msw_synchronize,
+    // destroyed with the context if the caller has not)
+    std::vector<hipStream_t> user_streams;
     // timing events of msw_align_reads_device launches not yet harvested
     struct DevTiming {
         hipEvent_t k0, k1;
@@ -1574,8 +1583,14 @@ void msw_ctx_destroy(msw_ctx* ctx) {
     (void)hipFree(ctx->c_s1);
     (void)hipFree(ctx->c_s2);
     (void)hipFree(ctx->c_res);
-    (void)hipFree(ctx->r_wins);
-    (void)hipFree(ctx->r_wlen);
+    for (auto& r : ctx->rscratch) {
+        (void)hipFree(r.wins);
+        (void)hipFree(r.wlen);
+    }
+    for (hipStream_t st : ctx->user_streams) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+    }
     for (auto& t : ctx->dev_timings) {
         (void)hipEventDestroy(t.k0);
         (void)hipEventDestroy(t.k1);
@@ -2017,21 +2032,29 @@ int msw_align_reads_device(msw_ctx* ctx, const msw_scoring_t* sc, const msw_geno
     harvest_dev_timings(ctx, false);
     const uint32_t ws = std::max<uint32_t>(16u, (max_win + 15u) & ~15u);
     const size_t wbytes = (size_t)n * ws;
-    if (wbytes > ctx->r_wins_cap) {
-        if ((rc = grow_dev(&ctx->r_wins, wbytes + wbytes / 4))) return rc;
-        ctx->r_wins_cap = wbytes + wbytes / 4;
+    msw_ctx::ReadsScratch* rs = nullptr;
+    for (auto& r : ctx->rscratch)
+        if (r.st == st) rs = &r;
+    if (!rs) {
+        ctx->rscratch.emplace_back();
+        rs = &ctx->rscratch.back();
+        rs->st = st;
+    }
+    if (wbytes > rs->wins_cap) {
+        if ((rc = grow_dev(&rs->wins, wbytes + wbytes / 4))) return rc;
+        rs->wins_cap = wbytes + wbytes / 4;
     }
     uint16_t* wlen = win_len_out;
     if (!wlen) {
-        if (n > ctx->r_wlen_cap) {
-            if ((rc = grow_dev(&ctx->r_wlen, (size_t)n + n / 4))) return rc;
-            ctx->r_wlen_cap = (size_t)n + n / 4;
+        if (n > rs->wlen_cap) {
+            if ((rc = grow_dev(&rs->wlen, (size_t)n + n / 4))) return rc;
+            rs->wlen_cap = (size_t)n + n / 4;
         }
-        wlen = ctx->r_wlen;
+        wlen = rs->wlen;
     }
-    HIP_TRY(msw::launch_cut_windows_for_reads(g->d_seq, g->len, win_pos, read_len, window, ctx->r_wins, wlen, ws, n,
+    HIP_TRY(msw::launch_cut_windows_for_reads(g->d_seq, g->len, win_pos, read_len, window, rs->wins, wlen, ws, n,
                                               st));
-    msw_batch_t b{reads, ctx->r_wins, read_len, wlen, read_stride, ws, n};
+    msw_batch_t b{reads, rs->wins, read_len, wlen, read_stride, ws, n};
     msw_ctx::DevTiming t{take_event(ctx), take_event(ctx), n};
     if (!t.k0 || !t.k1) return fail(MSW_E_DEVICE, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(t.k0, st));
@@ -2198,7 +2221,41 @@ int msw_synchronize(msw_ctx* ctx) {
     if (rc) return rc;
     for (hipStream_t st : {ctx->compute, ctx->compute2, ctx->copy, ctx->d2h, ctx->side})
         if (st) HIP_TRY(hipStreamSynchronize(st));
+    for (hipStream_t st : ctx->user_streams) HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipGetLastError());
+    return MSW_OK;
+}
+
+int msw_stream_create(msw_ctx* ctx, void** out) {
+    if (!ctx || !out) return fail(MSW_E_INVALID, "ctx/out is NULL");
+    *out = nullptr;
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    hipStream_t st = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    ctx->user_streams.push_back(st);
+    *out = st;
+    return MSW_OK;
+}
+
+int msw_stream_destroy(msw_ctx* ctx, void* stream) {
+    if (!ctx || !stream) return fail(MSW_E_INVALID, "ctx/stream is NULL");
+    auto it = std::find(ctx->user_streams.begin(), ctx->user_streams.end(), (hipStream_t)stream);
+    if (it == ctx->user_streams.end()) return fail(MSW_E_INVALID, "stream was not made by msw_stream_create on this context");
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    ctx->user_streams.erase(it);
+    // its per-stream scratch goes too (a later stream may reuse the handle)
+    for (size_t i = 0; i < ctx->rscratch.size(); ++i)
+        if (ctx->rscratch[i].st == (hipStream_t)stream) {
+            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+            (void)hipFree(ctx->rscratch[i].wins);
+            (void)hipFree(ctx->rscratch[i].wlen);
+            ctx->rscratch.erase(ctx->rscratch.begin() + (long)i);
+            break;
+        }
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
     return MSW_OK;
 }
 

@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
                    (fn_t)msw_memcpy_h2d, (fn_t)msw_memcpy_d2h, (fn_t)msw_synchronize,
                    (fn_t)msw_last_error, (fn_t)msw_version, (fn_t)msw_fastq_open,
                    (fn_t)msw_fastq_close, (fn_t)msw_fastq_next, (fn_t)msw_fastq_stats,
-                   (fn_t)msw_fastq_count_bases};
+                   (fn_t)msw_fastq_count_bases, (fn_t)msw_stream_create, (fn_t)msw_stream_destroy};
     size_t k;
     const int gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
     int n = -1;
@@ -42,6 +42,8 @@ int main(int argc, char** argv) {
     CHECK(msw_device_count(NULL) == MSW_E_INVALID);
     CHECK(msw_ctx_create(0, NULL) == MSW_E_INVALID);
     CHECK(msw_ctx_create_ex(0, MSW_CTX_LEAN, NULL) == MSW_E_INVALID);
+    CHECK(msw_stream_create(NULL, NULL) == MSW_E_INVALID);
+    CHECK(msw_stream_destroy(NULL, NULL) == MSW_E_INVALID);
     CHECK(msw_align_batch(NULL, NULL, NULL, NULL, 0) == MSW_E_INVALID);
     CHECK(strlen(msw_last_error()) > 0);
     CHECK(msw_fastq_open("/nonexistent.fastq.gz", NULL) == MSW_E_INVALID);
@@ -76,6 +78,23 @@ int main(int argc, char** argv) {
             score = 0;
             CHECK(msw_align_batch_async(ctx, &sc, &b, &o, 0, &t) == MSW_OK && msw_wait(ctx, t) == MSW_OK);
             CHECK(score == 12 && ei == 7 && ej == 6);
+        }
+        {
+            /* a stream of the caller's: a copy and a fence on it */
+            void* st = NULL;
+            uint64_t f = 0;
+            uint8_t back[16] = {0};
+            void* d = msw_dev_alloc(ctx, 16);
+            CHECK(d != NULL);
+            CHECK(msw_stream_create(ctx, &st) == MSW_OK && st != NULL);
+            CHECK(msw_memcpy_h2d(ctx, d, read, 16) == MSW_OK);
+            CHECK(msw_memcpy_d2h_async(ctx, back, d, 16, st) == MSW_OK);
+            CHECK(msw_fence_record(ctx, st, &f) == MSW_OK && msw_fence_wait(ctx, f) == MSW_OK);
+            CHECK(memcmp(back, read, 16) == 0);
+            CHECK(msw_synchronize(ctx) == MSW_OK);
+            CHECK(msw_stream_destroy(ctx, st) == MSW_OK);
+            CHECK(msw_stream_destroy(ctx, st) == MSW_E_INVALID); /* no longer this context's */
+            msw_dev_free(ctx, d);
         }
         msw_ctx_destroy(ctx);
     }
