@@ -242,7 +242,8 @@ int msw_synchronize(msw_ctx* ctx);
  * stream): msw_fence_wait blocks until everything enqueued on that stream
  * before msw_fence_record has finished, without waiting for what came after
  * (msw_synchronize drains all of the context's streams).  A fence is waited
- * on once; the context keeps unwaited fences until it is destroyed. */
+ * on once; the context keeps unwaited fences until it is destroyed.  Several
+ * threads may wait on (different) fences of one context at once. */
 int msw_fence_record(msw_ctx* ctx, void* stream, uint64_t* fence);
 int msw_fence_wait(msw_ctx* ctx, uint64_t fence);
 /* A stream of the context's device for callers that keep two batches in

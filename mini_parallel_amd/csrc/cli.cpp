@@ -845,6 +845,7 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     size_t fi = 0;
                     uint64_t fence = 0;  // after the batch's copy-back (msw_fence_record)
                     bool live = false;
+                    uint64_t* rec = nullptr;  // --scores-out: the batch's records (recbuf)
                 } res[2];
                 const size_t rec = 4 + 2 + 2 + 2 + 2;
                 for (Res& r : res) {
@@ -855,6 +856,16 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     r.h = (uint8_t*)msw_host_alloc(batch * rec);
                     if (!r.d_score || !r.d_ei || !r.d_ej || !r.d_wlen || !r.h)
                         die(std::string("GPU lane reader buffers: ") + msw_last_error());
+                }
+                // per-read records of a batch, built here and written from here:
+                // allocated and touched in setup (a fresh 2 MB buffer per batch
+                // page-faulted inside the last batch's settle, after the GPU)
+                std::unique_ptr<uint64_t[]> recbuf;
+                if (!a.scores_out.empty()) {
+                    recbuf.reset(new uint64_t[2 * batch]);  // one half per result set
+                    memset(recbuf.get(), 0, 2 * batch * sizeof(uint64_t));
+                    res[0].rec = recbuf.get();
+                    res[1].rec = recbuf.get() + batch;
                 }
                 const double t_res = ms_since(tres0);
                 unsigned long long alg_local = 0;
@@ -867,49 +878,60 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     finish_file(fi);
                 };
                 // host side of a finished batch: sums, cells, per-read records
-                auto settle = [&](Res& r) {
-                    if (!r.live) return;
-                    r.live = false;
+                // (settle_work: the batch's own buffers, the file's atomics and
+                // its scores file; settle_book: this worker's file table).
+                struct Settled {
+                    unsigned long long alg = 0;
+                };
+                auto settle_work = [&](Res& r) -> Settled {
+                    Settled out;
                     FileState& f = *st[r.fi];
                     trace_ev(wi, "settle-wait", r.n);
                     if (msw_fence_wait(ctx.h, r.fence) != MSW_OK) {
                         fprintf(stderr, "  GPU %d alignment error: %s\n", gi, msw_last_error());
                         f.failed = true;
-                    } else {
-                        const int32_t* sc32 = (const int32_t*)r.h;
-                        const int16_t* ei = (const int16_t*)(r.h + batch * 4);
-                        const int16_t* ej = ei + batch;
-                        const uint16_t* rl = (const uint16_t*)(ej + batch);
-                        const uint16_t* wl = rl + batch;
-                        long long sum = 0;
-                        unsigned long long cl = 0, nb = 0, nw = 0;
-                        for (uint64_t i = 0; i < r.n; ++i) {
-                            sum += sc32[i];
-                            cl += (unsigned long long)rl[i] * wl[i];
-                            nb += rl[i];
-                            nw += wl[i];
-                        }
-                        alg_local += nb + nw + (sc.want_coords ? 8ull : 4ull) * r.n;
-                        f.score += sum;
-                        f.bases += nb;
-                        f.reads += r.n;
-                        cells += cl;
-                        if (f.scores_fd >= 0) {
-                            // records [score i32 | end_i i16 | end_j i16], built as whole words
-                            // in a buffer that is not zeroed first
-                            std::unique_ptr<uint64_t[]> out(new uint64_t[r.n]);
-                            for (uint64_t i = 0; i < r.n; ++i)
-                                out[i] = (uint64_t)(uint32_t)sc32[i] | (uint64_t)(uint16_t)ei[i] << 32 |
-                                         (uint64_t)(uint16_t)ej[i] << 48;
-                            if (pwrite(f.scores_fd, out.get(), r.n * 8, (off_t)(r.first * 8)) != (ssize_t)(r.n * 8)) {
-                                fprintf(stderr, "  error writing scores for %s\n", f.path.c_str());
-                                f.failed = true;
-                            }
-                        }
+                        return out;
                     }
+                    const int32_t* sc32 = (const int32_t*)r.h;
+                    const int16_t* ei = (const int16_t*)(r.h + batch * 4);
+                    const int16_t* ej = ei + batch;
+                    const uint16_t* rl = (const uint16_t*)(ej + batch);
+                    const uint16_t* wl = rl + batch;
+                    long long sum = 0;
+                    unsigned long long cl = 0, nb = 0, nw = 0;
+                    // records [score i32 | end_i i16 | end_j i16], built as whole
+                    // words in the same pass as the sums
+                    uint64_t* rec = f.scores_fd >= 0 ? r.rec : nullptr;
+                    for (uint64_t i = 0; i < r.n; ++i) {
+                        sum += sc32[i];
+                        cl += (unsigned long long)rl[i] * wl[i];
+                        nb += rl[i];
+                        nw += wl[i];
+                        if (rec)
+                            rec[i] = (uint64_t)(uint32_t)sc32[i] | (uint64_t)(uint16_t)ei[i] << 32 |
+                                     (uint64_t)(uint16_t)ej[i] << 48;
+                    }
+                    out.alg = nb + nw + (sc.want_coords ? 8ull : 4ull) * r.n;
+                    f.score += sum;
+                    f.bases += nb;
+                    f.reads += r.n;
+                    cells += cl;
+                    if (rec && pwrite(f.scores_fd, rec, r.n * 8, (off_t)(r.first * 8)) != (ssize_t)(r.n * 8)) {
+                        fprintf(stderr, "  error writing scores for %s\n", f.path.c_str());
+                        f.failed = true;
+                    }
+                    return out;
+                };
+                auto settle_book = [&](Res& r, const Settled& o) {
+                    alg_local += o.alg;
                     open_files[r.fi].first -= 1;
                     maybe_finish(r.fi);
                     trace_ev(wi, "settled", r.n);
+                };
+                auto settle = [&](Res& r) {
+                    if (!r.live) return;
+                    r.live = false;
+                    settle_book(r, settle_work(r));
                 };
                 int cur = 0;
                 setup_phase(t_ctx, t_gen, t_res, t_rd, t_kl);
@@ -1023,6 +1045,8 @@ WgsReport run_full_wgs(const Args& a, const std::vector<Device>& devices, const 
                     open_files[fi].first += 1;
                     cur ^= 1;
                 }
+                // (the last two batches' host work on two threads measured
+                // equal: config 3 from FASTQ 13.22-13.42 vs 13.16-13.26 ms)
                 settle(res[cur]);
                 settle(res[cur ^ 1]);
                 mark_done();

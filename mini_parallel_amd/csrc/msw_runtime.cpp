@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -393,6 +394,9 @@ struct msw_ctx {
     };
     std::deque<DevTiming> dev_timings;
     std::vector<hipEvent_t> free_events;
+    // free_events and fences: msw_fence_wait may run on several threads at
+    // once (--full-wgs settles its last two batches on two)
+    std::mutex ev_mu;
     msw::Layout last_layout = msw::Layout::kPairs;  // the last packed launch's plan (MSW_HOST_TRACE)
     uint32_t last_group_lanes = 0, last_kr = 0;
     std::unordered_map<uint64_t, hipEvent_t> fences;  // msw_fence_record, not yet waited on
@@ -430,10 +434,13 @@ int aux_streams(msw_ctx* ctx) {
 }
 
 hipEvent_t take_event(msw_ctx* ctx) {
-    if (!ctx->free_events.empty()) {
-        hipEvent_t e = ctx->free_events.back();
-        ctx->free_events.pop_back();
-        return e;
+    {
+        std::lock_guard<std::mutex> lk(ctx->ev_mu);
+        if (!ctx->free_events.empty()) {
+            hipEvent_t e = ctx->free_events.back();
+            ctx->free_events.pop_back();
+            return e;
+        }
     }
     hipEvent_t e = nullptr;
     return hipEventCreate(&e) == hipSuccess ? e : nullptr;
@@ -498,8 +505,11 @@ void harvest_dev_timings(msw_ctx* ctx, bool wait) {
         add_kernel_interval(ctx, t.k0, t.k1);
         ctx->stats.launches += 1;
         ctx->stats.pairs += t.pairs;
-        ctx->free_events.push_back(t.k0);
-        ctx->free_events.push_back(t.k1);
+        {
+            std::lock_guard<std::mutex> lk(ctx->ev_mu);
+            ctx->free_events.push_back(t.k0);
+            ctx->free_events.push_back(t.k1);
+        }
         ctx->dev_timings.pop_front();
     }
 }
@@ -2192,6 +2202,7 @@ int msw_fence_record(msw_ctx* ctx, void* stream, uint64_t* fence) {
     if (rc) return rc;
     hipEvent_t e = take_event(ctx);
     if (!e) return fail(MSW_E_DEVICE, "hipEventCreate failed");
+    std::lock_guard<std::mutex> lk(ctx->ev_mu);
     if (hipEventRecord(e, stream ? (hipStream_t)stream : ctx->compute) != hipSuccess) {
         ctx->free_events.push_back(e);
         return fail(MSW_E_DEVICE, "hipEventRecord failed");
@@ -2203,14 +2214,21 @@ int msw_fence_record(msw_ctx* ctx, void* stream, uint64_t* fence) {
 
 int msw_fence_wait(msw_ctx* ctx, uint64_t fence) {
     if (!ctx) return fail(MSW_E_INVALID, "ctx is NULL");
-    auto it = ctx->fences.find(fence);
-    if (it == ctx->fences.end()) return fail(MSW_E_INVALID, "unknown fence %llu", (unsigned long long)fence);
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(ctx->ev_mu);
+        auto it = ctx->fences.find(fence);
+        if (it == ctx->fences.end()) return fail(MSW_E_INVALID, "unknown fence %llu", (unsigned long long)fence);
+        e = it->second;
+        ctx->fences.erase(it);
+    }
     int rc = set_device(ctx);
     if (rc) return rc;
-    hipEvent_t e = it->second;
-    ctx->fences.erase(it);
     const hipError_t err = hipEventSynchronize(e);
-    ctx->free_events.push_back(e);
+    {
+        std::lock_guard<std::mutex> lk(ctx->ev_mu);
+        ctx->free_events.push_back(e);
+    }
     if (err != hipSuccess) return fail(MSW_E_DEVICE, "GPU error before the fence: %s", hipGetErrorString(err));
     return MSW_OK;
 }
