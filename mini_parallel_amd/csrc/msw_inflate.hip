@@ -743,10 +743,11 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     // lane by pointer jumping -- and one ring write stores the
                     // window's W bytes.  Windows of more than 64 output bytes take
                     // the serial walk.
-                    // (a lane whose token is not simple: next lane 255, length 0)
+                    // (a lane L whose token is not simple: "next lane" 192 + L, length
+                    // 0 -- past any simple token's next lane, <= 111, and it names L)
                     uint32_t nx_lit = (lane + (e & 15u)) | (((e >> 4) & 3u) << 8), nx_mat = (lane + tm) | (len << 8);
                     asm volatile("" : "+v"(nx_lit), "+v"(nx_mat));  // both on every lane, then selects
-                    const uint32_t nxo = m_lit ? nx_lit : (m_mat ? nx_mat : 255u);
+                    const uint32_t nxo = m_lit ? nx_lit : (m_mat ? nx_mat : 192u + lane);
                     // The chain's first token starts the window: every lane takes
                     // it.  A later token's record carries its first byte W in bits
                     // 5:0 (OR'd on the scalar unit; W < 64 for every token of a
@@ -755,18 +756,16 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     uint32_t ti = (uint32_t)__builtin_amdgcn_readlane((int)info, 0);
                     uint32_t W = t >> 8;
                     // one exit: k leaves the window (>= 64) or hits a token that
-                    // is not simple (255; the token at kp, which added nothing)
-                    uint32_t kp = 0;
+                    // is not simple (k = 192 + its lane; it added nothing)
                     k = t & 255u;
                     while (k < 64) {
                         t = (uint32_t)__builtin_amdgcn_readlane((int)nxo, (int)k);
                         const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k) | W;
                         ti = lane >= W ? s0 : ti;
                         W += t >> 8;
-                        kp = k;
                         k = t & 255u;
                     }
-                    if (k == 255u) k = kp;
+                    if (k >= 192u) k -= 192u;
                     if (W <= 64u) {
                         if (W) {
                             // offset in the token: lane - its first byte (ti's bits 5:0)
