@@ -100,6 +100,15 @@ __device__ __forceinline__ uint32_t vbfe(uint32_t v, uint32_t off, uint32_t wid)
     return d;
 }
 
+// v_readlane_b32 with the lane select held in the SGPR given (the builtin
+// lets the compiler substitute any value with the same low 6 bits, which in
+// the walk kept an extra copy of the record live: one s_mov per token)
+__device__ __forceinline__ uint32_t readlane_s(uint32_t v, uint32_t lane_sel) {
+    uint32_t d;
+    asm("v_readlane_b32 %0, %1, %2" : "=s"(d) : "v"(v), "s"(lane_sel));
+    return d;
+}
+
 __device__ __forceinline__ uint32_t len_base(uint32_t sym, uint32_t& extra) {
     if (sym < 265) { extra = 0; return sym - 254; }
     if (sym < 285) { extra = (sym - 261) >> 2; return ((4u + ((sym - 265) & 3u)) << extra) + 3u; }
@@ -759,8 +768,8 @@ __global__ __launch_bounds__(64, inflate_waves<RING>()) void gz_inflate_kernel(c
                     // is not simple (k = 192 + its lane; it added nothing)
                     k = t & 255u;
                     while (k < 64) {
-                        t = (uint32_t)__builtin_amdgcn_readlane((int)nxo, (int)k);
-                        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)k) | W;
+                        t = readlane_s(nxo, k);
+                        const uint32_t s0 = readlane_s(info, k) | W;
                         ti = lane >= W ? s0 : ti;
                         W += t >> 8;
                         k = t & 255u;
